@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X DCT codec hot path (BASELINE.json `metric`).
+
+A step = one DCT compress + decompress round trip of one 4032x3008 IYUV frame
+(BASELINE.json configs[1]: chef-with-trumpet-big, q=50; its raw input is
+missing from the reference, so the frame is the decode of
+chef-with-trumpet-big-DCT-50.myyuv, sha-pinned), with the frame and the
+compressed stream resident in HBM: compress_device -> decompress_device on one
+stream.  value = megapixels (luma W*H) of all ranks' steps / max-over-ranks
+wall time of the K timed steps.
+
+roofline: K1 fdct_quant_zz (the block-transform kernel of the north star),
+algorithmic bytes = 3 B per sample (1 B u8 in + 2 B int16 out) x W*H*3/2
+samples per launch, divided by its average launch time from HIP events on the
+launch stream over the timed region.  `traffic` = FETCH_SIZE*2 + WRITE_SIZE
+per launch from a rocprofv3 --pmc run committed under profiles/ (null if none).
+
+cpu_baseline: the reference library itself (oracle/_ref, built from the
+reference sources with OpenMP, kind "reference") — or the C restatement
+(oracle/, kind "port") when _ref is absent — timed on this box's host cores,
+rank 0 at N=1 only, on a bounded sample of the same workload.
+
+N>1 (torch.distributed.run, one rank per GPU): frames are sharded one per GPU
+(weak scaling); at the end of the timed region rank 0 gathers every rank's
+compressed streams over RCCL (sizes all-gathered first, then exact-size
+point-to-point transfers): the batch configuration's exchange step.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "yuv-manipulations-2_amd")
+sys.path[:0] = [ROOT, PKG]
+
+GOLDEN_BIG = os.path.join(ROOT, "tests", "golden", "chef-with-trumpet-big-DCT-50.myyuv")
+BIG_DECODED_SHA = "5e7769191188285cc127c6b4da900b3420f064191f707383c82128c14e497e5c"
+BIG_RECOMPRESSED_SHA = "fe9b7317653c2b44a9f24436f0e349b083b4e368cf9653e8777e9f7a79cebfcc"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8 TB/s spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--quality", type=int, default=50)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="budget of the cpu_baseline sample (0 disables it)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or nproc")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="time the step without per-kernel HIP events")
+    return ap.parse_args()
+
+
+def load_traffic():
+    """Per-launch HBM bytes of K1 from the newest profiles/*traffic*.json."""
+    pdir = os.path.join(ROOT, "profiles")
+    best = None
+    if os.path.isdir(pdir):
+        for n in sorted(os.listdir(pdir)):
+            if n.endswith(".json") and "traffic" in n:
+                best = os.path.join(pdir, n)
+    if not best:
+        return None
+    try:
+        with open(best) as f:
+            d = json.load(f)
+        return d.get("fdct_quant_zz", {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(raw, w, h, q, seconds, threads):
+    """Reference OpenMP build (or the C restatement) on the host cores."""
+    ncpu = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    os.environ["OMP_NUM_THREADS"] = str(ncpu)
+    mp = w * h / 1e6
+    try:
+        from oracle import ref as R
+        if R.available("omp"):
+            tc, td = R.bench(raw, w, h, (q, q, q), 1)
+            iters = max(3, min(64, int(seconds / max(1e-3, (tc + td) / 1e3))))
+            tc, td = R.bench(raw, w, h, (q, q, q), iters)
+            return {"value": round(mp / ((tc + td) / 1e3), 2), "unit": "MP/s", "cores": ncpu,
+                    "kind": "reference",
+                    "sample": f"{iters} in-process compress+decompress round trips of the "
+                              f"{w}x{h} q{q} frame (median; reference myyuv_lib -O3 OpenMP, "
+                              f"compress {tc:.1f} ms + decompress {td:.1f} ms)"}
+    except Exception as e:  # fall back to the restatement
+        log("cpu_baseline: reference build unavailable:", e)
+    from oracle import oracle as O
+    O.set_num_threads(ncpu)
+    t0 = time.perf_counter()
+    pay = O.compress(raw, w, h, (q, q, q))
+    O.decompress(pay, w, h, (q, q, q))
+    one = time.perf_counter() - t0
+    iters = max(3, min(64, int(seconds / max(one, 1e-3))))
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        pay = O.compress(raw, w, h, (q, q, q))
+        O.decompress(pay, w, h, (q, q, q))
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    t = ts[len(ts) // 2]
+    return {"value": round(mp / t, 2), "unit": "MP/s", "cores": ncpu, "kind": "port",
+            "sample": f"{iters} compress+decompress round trips of the {w}x{h} q{q} frame "
+                      f"(median; C restatement -O2 OpenMP)"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import myyuv_hip
+    import myyuv_file
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    codec = myyuv_hip.Codec(local)
+
+    # ---- workload: the decoded big golden frame (sha-pinned)
+    g = myyuv_file.YUVFile.load(GOLDEN_BIG)
+    w, h, q = g.width, g.height, args.quality
+    raw = codec.decompress(g.data, w, h, tuple(g.params))
+    if hashlib.sha256(g.decompressed(raw).dumps()).hexdigest() != BIG_DECODED_SHA:
+        raise SystemExit("decoded chef-big frame does not match its pinned sha")
+    mp = w * h / 1e6
+    samples = w * h * 3 // 2
+    cap = myyuv_hip.payload_bound(w, h)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    d_in = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+    d_out = torch.empty(samples, dtype=torch.uint8, device=dev)
+    # one payload slot per timed step: the batch of compressed streams this
+    # rank contributes (gathered to rank 0 at N>1)
+    nslot = max(1, args.steps)
+    d_pay = torch.empty((nslot, cap), dtype=torch.uint8, device=dev)
+    d_size = torch.zeros(nslot, dtype=torch.int32, device=dev)
+    codec.reserve(w, h)
+
+    def step(i):
+        codec.compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay[i].data_ptr(), cap,
+                              d_size[i:i + 1].data_ptr(), sp)
+        codec.decompress_device(d_pay[i].data_ptr(), d_size[i:i + 1].data_ptr(), cap, w, h,
+                                (q, q, q), d_out.data_ptr(), sp)
+
+    for i in range(args.warmup):
+        step(i % nslot)
+    rc, bad = codec.sync_status(sp)
+    if rc:
+        raise SystemExit(f"codec error {rc} ({myyuv_hip.strerror(rc)}) at block {bad}")
+    n0 = int(d_size[0].item())
+    pay0 = bytes(d_pay[0, :n0].cpu().numpy())
+    if q == 50 and hashlib.sha256(pay0).hexdigest() != BIG_RECOMPRESSED_SHA:
+        raise SystemExit("compressed stream differs from the pinned reference bytes")
+    if bytes(d_out.cpu().numpy()) != codec.decompress(pay0, w, h, (q, q, q)):
+        raise SystemExit("device round trip differs from the host-API decode")
+
+    # ---- timed region
+    if not args.no_kernel_events:
+        codec.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i % nslot)
+    gathered = None
+    if world > 1:
+        gathered = gather_streams(dist, d_pay, d_size, args.steps, world, rank, dev)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    rc, bad = codec.sync_status(sp)
+    if rc:
+        raise SystemExit(f"codec error {rc} ({myyuv_hip.strerror(rc)}) at block {bad}")
+    stats = codec.kernel_stats() if not args.no_kernel_events else {}
+    codec.profile(False)
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+        if rank == 0:
+            assert gathered == world * args.steps, gathered
+
+    if rank == 0:
+        ms_step = t / args.steps * 1e3
+        value = world * args.steps * mp / t
+        k1_ms, k1_n = stats.get("fdct_quant_zz", (0.0, 0))
+        roof = None
+        if k1_n:
+            avg_s = k1_ms / k1_n / 1e3
+            alg = 3 * samples
+            achieved = alg / avg_s / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": load_traffic(), "kernel": "fdct_quant_zz",
+                    "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2)}
+        for k, (kms, kn) in stats.items():
+            if kn:
+                log(f"kernel {k:14s} {kms / kn * 1e3:9.2f} us/launch  x{kn}")
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(raw, w, h, q, args.cpu_seconds, args.cpu_threads)
+        line = {
+            "metric": "megapixels/sec DCT compress+decompress, 4K IYUV; achieved HBM GB/s vs peak",
+            "value": round(value, 2), "unit": "MP/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8/int16 (fp32 transform)",
+            "data": "chef-with-trumpet-big-DCT-50.myyuv decoded (4032x3008 IYUV, sha-pinned); "
+                    "stand-in for the missing raw 4K",
+            "config": {"workload": f"chef-with-trumpet-big 4032x3008 IYUV DCT q={q} "
+                                   f"compress+decompress, HBM-resident, 1 frame/step/GPU",
+                       "frame": f"{w}x{h}", "quality": q, "parallelism": f"frames sharded, dp{world}",
+                       "payload_bytes": n0},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    codec.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def gather_streams(dist, d_pay, d_size, steps, world, rank, dev):
+    """RCCL gather of every rank's compressed streams to rank 0: all-gather the
+    u32 sizes, then exact-size point-to-point sends (batched in one group)."""
+    import torch
+    sizes = torch.empty((world, steps), dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(sizes, d_size[:steps].contiguous())
+    hs = sizes.cpu().tolist()
+    ops = []
+    recv = []
+    if rank == 0:
+        for r in range(1, world):
+            for i in range(steps):
+                buf = torch.empty(hs[r][i], dtype=torch.uint8, device=dev)
+                recv.append(buf)
+                ops.append(dist.P2POp(dist.irecv, buf, r))
+    else:
+        for i in range(steps):
+            ops.append(dist.P2POp(dist.isend, d_pay[i, :hs[rank][i]], 0))
+    if ops:
+        for rq in dist.batch_isend_irecv(ops):
+            rq.wait()
+    return world * steps if rank == 0 else 0
+
+
+if __name__ == "__main__":
+    main()

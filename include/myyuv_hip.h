@@ -1,0 +1,131 @@
+/*
+ * myyuv_hip.h — C ABI of the MI355X (gfx950) DCT codec: the drop-in boundary
+ * for the reference's DCT compress/decompress path.
+ *
+ * The reference binds this path in two places (paths relative to
+ * /root/reference/myyuv_lib/):
+ *   - myyuv_yuv.hpp:111,116 / myyuv_yuv.cpp:130-160: YUV::compress_map[DCT][IYUV]
+ *     and YUV::decompress_map[DCT][IYUV] (std::function plugin table), and
+ *   - myyuv_DCT/DCT.hpp:16,25 (extern-declared at myyuv_yuv.cpp:9-14):
+ *     myyuvDCT::compress_DCT_planar / decompress_DCT_planar.
+ * Each entry point below says which of those it replaces.  The C++ adapter
+ * that re-registers the maps through this ABI is
+ * yuv-manipulations-2_amd/csrc/host/myyuv_yuv.cpp.
+ *
+ * Byte format: the payload handled here is exactly the DCTYUV stream the
+ * reference writes after the 64-byte YUVHeader and the 3 quality bytes
+ * (DCT.cpp:112-197, Huffman.cpp:279-326): u32 plane_size[3],
+ * then per plane u32 nblocks, u32 content_size, u8 chunk_size[nblocks],
+ * u8 content[content_size].  Frames are IYUV (4:2:0 planar, Y then U then V).
+ *
+ * Plain pointers and sizes only; no torch or HIP types in the signatures
+ * (streams are passed as void* = hipStream_t).  All functions return 0 or a
+ * MYYUV_E_* code; myyuv_hip_strerror() gives the reference's message for it.
+ */
+#ifndef MYYUV_HIP_H
+#define MYYUV_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes.  The string for each (myyuv_hip_strerror) is the exact
+ * std::runtime_error text the reference throws at the cited line. */
+#define MYYUV_OK 0
+#define MYYUV_E_ARG 1             /* null pointer / bad handle (no reference counterpart) */
+#define MYYUV_E_QUALITY 2         /* DCT.cpp:380,440 "Level of quality must be between 1 and 100" */
+#define MYYUV_E_WIDTH 3           /* DCT.cpp:281,339 "Error. width % 8 must be 0" */
+#define MYYUV_E_HEIGHT 4          /* DCT.cpp:284,342 "Error. height % 8 must be 0" */
+#define MYYUV_E_CAPACITY 5        /* output buffer smaller than the payload (no reference counterpart) */
+#define MYYUV_E_DCTYUV_SIZE 6     /* DCT.cpp:133,144 "DCTYUV load bad size" */
+#define MYYUV_E_PLANE_SIZE 7      /* DCT.cpp:42,54 "DCTYUVPlane load bad size" */
+#define MYYUV_E_PLANE_NBLK 8      /* DCT.cpp:48 "DCTYUVPlane load chunks_sizes_size bad size" */
+#define MYYUV_E_PLANE_CONTENT 9   /* DCT.cpp:51 "DCTYUVPlane load content_size bad size" */
+#define MYYUV_E_BAD_CODE 10       /* Huffman.cpp:121,130 "Huffman bad code" */
+#define MYYUV_E_UNKNOWN_SYMBOL 11 /* Huffman.cpp:139 "Huffman unknown symbol" */
+#define MYYUV_E_BAD_CHUNK 12      /* malformed chunk header/table (reference: assert / UB) */
+#define MYYUV_E_HIP 13            /* HIP runtime failure */
+#define MYYUV_E_NO_DEVICE 14      /* no gfx950 device / HIP unavailable */
+
+typedef struct myyuv_hip_ctx* myyuv_hip_handle;
+
+/* Context: one per (host thread, device).  Owns a HIP stream, the per-call
+ * workspace (grown on demand, never freed inside a call) and pinned staging
+ * buffers for the host-buffer entry points.  Reentrant across contexts, as the
+ * reference is (SURVEY.md §8b "Threading"). */
+int myyuv_hip_create(int device, myyuv_hip_handle* out);
+void myyuv_hip_destroy(myyuv_hip_handle h);
+const char* myyuv_hip_strerror(int code);
+
+/* Upper bound of the DCTYUV payload for a WxH IYUV frame (worst-case 160 B per
+ * 8x8 block + headers); size the compress output buffer with it. */
+uint32_t myyuv_dct_payload_bound(uint32_t width, uint32_t height);
+
+/* Host-buffer compress: replaces myyuvDCT::compress_DCT_planar's data path
+ * (DCT.cpp:371-430), i.e. what YUV::compress_map[DCT][IYUV] runs
+ * (myyuv_yuv.cpp:132-142).  iyuv = W*H*3/2 bytes (Y, U, V planes as in
+ * YUV::getYUVPlanes, myyuv_yuv.cpp:383-423).  Writes the DCTYUV payload to
+ * `payload` (capacity `cap`) and its size to *payload_size.  The caller (C++
+ * adapter) writes the 64-B header and the 3 quality bytes. */
+int myyuv_gpu_dct_compress(myyuv_hip_handle h, const uint8_t* iyuv, uint32_t width,
+                           uint32_t height, const uint8_t quality[3], uint8_t* payload,
+                           uint32_t cap, uint32_t* payload_size);
+
+/* Host-buffer decompress: replaces myyuvDCT::decompress_DCT_planar's data path
+ * (DCT.cpp:432-488), what YUV::decompress_map[DCT][IYUV] runs
+ * (myyuv_yuv.cpp:148-158).  Writes W*H*3/2 bytes to `iyuv`.  On a decode error
+ * returns its code; *bad_block (optional) receives the global block index
+ * (plane-major, row-major blocks) of the first failing block, -1 for header
+ * errors. */
+int myyuv_gpu_dct_decompress(myyuv_hip_handle h, const uint8_t* payload, uint32_t size,
+                             uint32_t width, uint32_t height, const uint8_t quality[3],
+                             uint8_t* iyuv, int64_t* bad_block);
+
+/* Device-resident variants (HBM in, HBM out), asynchronous on `stream`
+ * (hipStream_t; NULL = the context's stream).  Used by the batch driver and
+ * the benchmark: no host synchronisation, no allocation once the workspace
+ * has grown to the frame size (call myyuv_hip_reserve first to pre-size it).
+ *   compress:   d_iyuv (W*H*3/2 B) -> d_payload (cap B), *d_payload_size (u32, device)
+ *   decompress: d_payload + *d_payload_size (device u32) -> d_iyuv
+ * Errors found on the device are collected in the context and returned by
+ * myyuv_hip_sync_status. */
+int myyuv_hip_reserve(myyuv_hip_handle h, uint32_t width, uint32_t height);
+int myyuv_gpu_dct_compress_device(myyuv_hip_handle h, const void* d_iyuv, uint32_t width,
+                                  uint32_t height, const uint8_t quality[3], void* d_payload,
+                                  uint32_t cap, uint32_t* d_payload_size, void* stream);
+int myyuv_gpu_dct_decompress_device(myyuv_hip_handle h, const void* d_payload,
+                                    const uint32_t* d_payload_size, uint32_t cap, uint32_t width,
+                                    uint32_t height, const uint8_t quality[3], void* d_iyuv,
+                                    void* stream);
+/* Waits for `stream`, returns (and clears) the first device-side error since
+ * the last call; *bad_block as above. */
+int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
+
+/* Per-kernel timing (HIP events around each launch, on the launch stream).
+ * enable=1 starts recording; myyuv_hip_kernel_stats fills, per kernel id
+ * (MYYUV_K_*), the summed milliseconds and launch count since enabling. */
+#define MYYUV_K_FDCT 0       /* K1 fdct_quant_zz */
+#define MYYUV_K_HUFF_ENC 1   /* K2 huff_encode */
+#define MYYUV_K_SCAN 2       /* scan of chunk sizes (both directions) */
+#define MYYUV_K_COMPACT 3    /* K4 compaction into the DCTYUV stream */
+#define MYYUV_K_PARSE 4      /* decode-side stream header parse */
+#define MYYUV_K_HUFF_DEC 5   /* K5 huff_decode */
+#define MYYUV_K_IDCT 6       /* K6 dequant_idct */
+#define MYYUV_K_COUNT 7
+int myyuv_hip_profile(myyuv_hip_handle h, int enable);
+int myyuv_hip_kernel_stats(myyuv_hip_handle h, double ms[MYYUV_K_COUNT],
+                           int64_t launches[MYYUV_K_COUNT]);
+
+/* Block-level entry points for known-answer tests (device round trip of one
+ * batch of blocks).  coef is zig-zag ordered int16[64] per block. */
+int myyuv_gpu_fdct_blocks(myyuv_hip_handle h, const uint8_t* px, uint32_t nblocks,
+                          const float qtable[64], int16_t* coef_zz);
+int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle h, const int16_t* coef_zz, uint32_t nblocks,
+                                 uint8_t* chunks160, uint8_t* sizes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MYYUV_HIP_H */

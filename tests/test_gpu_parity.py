@@ -1,0 +1,191 @@
+"""GPU parity: the HIP path (libmyyuv_hip.so through its C ABI) against the
+CPU restatement (oracle/), the reference's golden files, and — when the
+reference library built by oracle/Makefile is present — the reference itself.
+Integer/byte work: every comparison is bit-exact."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import blockgen
+
+pytestmark = pytest.mark.gpu
+
+SMALL_W, SMALL_H = 992, 736
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.mark.parametrize("q,gold", [(50, "chef-with-trumpet-DCT-50.myyuv"),
+                                    (90, "chef-with-trumpet-DCT-90.myyuv")])
+def test_golden_compress_small(codec, golden, q, gold):
+    raw = golden("chef-with-trumpet.myyuv")
+    g = golden(gold)
+    pay = codec.compress(raw.data, raw.width, raw.height, (q, q, q))
+    assert pay == g.data
+    # whole file, as myyuv_cli -compress writes it
+    assert sha(raw.compressed(bytes([q] * 3), pay).dumps()) == sha(g.dumps())
+
+
+@pytest.mark.parametrize("gold", ["chef-with-trumpet-DCT-50.myyuv", "chef-with-trumpet-DCT-90.myyuv"])
+def test_golden_decompress_small(codec, golden, oracle, gold):
+    g = golden(gold)
+    out = codec.decompress(g.data, g.width, g.height, tuple(g.params))
+    assert out == oracle.decompress(g.data, g.width, g.height, tuple(g.params))
+
+
+def test_golden_decompress_small_known_hash(codec, golden):
+    g = golden("chef-with-trumpet-DCT-50.myyuv")
+    out = codec.decompress(g.data, g.width, g.height, tuple(g.params))
+    assert sha(g.decompressed(out).dumps()) == \
+        "a95127da471524c1f7860c47d9b11e2c835ffa220c6d7aadf71e0fb6e45a9306"
+
+
+def test_golden_big_roundtrip(codec, golden, chef_big):
+    f, raw_oracle = chef_big
+    raw = codec.decompress(f.data, f.width, f.height, tuple(f.params))
+    assert raw == raw_oracle
+    dec_file = f.decompressed(raw)
+    assert sha(dec_file.dumps()) == "5e7769191188285cc127c6b4da900b3420f064191f707383c82128c14e497e5c"
+    pay = codec.compress(raw, f.width, f.height, (50, 50, 50))
+    assert len(pay) == 3363749
+    assert sha(pay) == "fe9b7317653c2b44a9f24436f0e349b083b4e368cf9653e8777e9f7a79cebfcc"
+    assert sha(dec_file.compressed(b"222", pay).dumps()) == \
+        "18405d3e6f79a0054fbdb166ae76f58d8dbffc605263f4c3c0b65e51babefbf7"
+
+
+@pytest.mark.parametrize("q", [1, 5, 25, 50, 51, 75, 90, 99, 100])
+def test_edge_frame_vs_oracle(codec, oracle, q):
+    w, h = 256, 128
+    fr = blockgen.edge_frame(w, h)
+    pay = codec.compress(fr.tobytes(), w, h, (q, q, q))
+    assert pay == oracle.compress(fr.tobytes(), w, h, (q, q, q))
+    assert codec.decompress(pay, w, h, (q, q, q)) == oracle.decompress(pay, w, h, (q, q, q))
+
+
+@pytest.mark.parametrize("q", [(50, 50, 50), (90, 90, 90), (100, 100, 100), (10, 60, 95)])
+def test_noise_vs_oracle(codec, oracle, q):
+    import synth
+    w, h = 512, 256
+    fr = synth.noise_frame(w, h)
+    pay = codec.compress(fr.tobytes(), w, h, q)
+    assert pay == oracle.compress(fr.tobytes(), w, h, q)
+    assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q)
+
+
+@pytest.mark.parametrize("wh", [(16, 16), (48, 16), (16, 48), (1008, 16), (144, 272)])
+def test_odd_geometries(codec, oracle, wh):
+    w, h = wh
+    rng = np.random.default_rng(w * 1000 + h)
+    fr = rng.integers(0, 256, w * h * 3 // 2).astype(np.uint8).tobytes()
+    for q in (20, 80):
+        pay = codec.compress(fr, w, h, (q, q, q))
+        assert pay == oracle.compress(fr, w, h, (q, q, q))
+        assert codec.decompress(pay, w, h, (q, q, q)) == oracle.decompress(pay, w, h, (q, q, q))
+
+
+def test_fdct_blocks_vs_oracle(codec, oracle):
+    rng = np.random.default_rng(3)
+    px = rng.integers(0, 256, (4096, 64)).astype(np.uint8)
+    px[:64] = 128
+    px[64:128] = 0
+    px[128:192] = 255
+    for q, chroma in ((1, 0), (50, 0), (90, 1), (100, 0)):
+        Q = oracle.qtable(q, chroma)
+        got = codec.fdct_blocks(px, Q)
+        zig = np.array([0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40,
+                        48, 41, 34, 27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29,
+                        22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
+                        47, 55, 62, 63])
+        for i in range(0, 4096, 97):
+            ref = oracle.fdct_block(px[i], Q)
+            assert np.array_equal(got[i], ref[zig]), (q, i)
+
+
+def test_huff_encode_edge_blocks(codec, oracle):
+    blocks = blockgen.edge_blocks()
+    coefs = np.stack([b for _, b in blocks])
+    chunks = codec.huff_encode_blocks(coefs)
+    from oracle.oracle import huff_encode_block
+    zz = np.array([0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48,
+                   41, 34, 27, 20, 13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15,
+                   23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63])
+    for (name, b), got in zip(blocks, chunks):
+        natural = np.zeros(64, np.int16)
+        natural[zz] = b  # zig-zag order -> natural order for the oracle API
+        assert got == huff_encode_block(natural), name
+
+
+def test_decode_errors_match_oracle(codec, oracle, golden):
+    import myyuv_hip
+    g = golden("chef-with-trumpet-DCT-50.myyuv")
+    w, h, q = g.width, g.height, tuple(g.params)
+    data = bytearray(g.data)
+    cases = {
+        "truncated": bytes(data[:100]),
+        "tiny": bytes(data[:8]),
+        "plane_size_zero": bytes(bytearray(b"\0\0\0\0") + data[4:]),
+    }
+    # corrupt the first chunk's nbits so its bits run out -> "Huffman bad code"
+    bad = bytearray(data)
+    nblk = int.from_bytes(bad[12:16], "little")
+    c0 = 12 + 8 + nblk
+    bad[c0] = 0xFF
+    bad[c0 + 1] = 0x01
+    cases["bad_nbits"] = bytes(bad)
+    bad2 = bytearray(data)
+    bad2[12 + 4: 12 + 8] = (1).to_bytes(4, "little")  # content_size too small
+    cases["content_small"] = bytes(bad2)
+    for name, pay in cases.items():
+        try:
+            oracle.decompress(pay, w, h, q)
+            exp = 0
+        except RuntimeError as e:
+            exp = e.args[0]
+        try:
+            codec.decompress(pay, w, h, q)
+            got = 0
+        except myyuv_hip.CodecError as e:
+            got = e.code
+        assert got == exp, (name, got, exp)
+
+
+def test_argument_errors(codec):
+    import myyuv_hip
+    fr = bytes(64 * 64 * 3 // 2)
+    with pytest.raises(myyuv_hip.CodecError) as e:
+        codec.compress(fr, 64, 64, (0, 50, 50))
+    assert e.value.code == myyuv_hip.E_QUALITY
+    assert str(e.value) == "Level of quality must be between 1 and 100"
+    with pytest.raises(myyuv_hip.CodecError) as e:
+        codec.compress(bytes(72 * 64 * 3 // 2), 72, 64, (50, 50, 50))
+    assert e.value.code == myyuv_hip.E_WIDTH
+    with pytest.raises(myyuv_hip.CodecError) as e:
+        codec.compress(bytes(64 * 40 * 3 // 2), 64, 40, (50, 50, 50))
+    assert e.value.code == myyuv_hip.E_HEIGHT
+
+
+def test_device_api_roundtrip(codec, golden):
+    import torch
+    import myyuv_hip
+    raw = golden("chef-with-trumpet.myyuv")
+    g = golden("chef-with-trumpet-DCT-50.myyuv")
+    w, h = raw.width, raw.height
+    cap = myyuv_hip.payload_bound(w, h)
+    d_in = torch.frombuffer(bytearray(raw.data), dtype=torch.uint8).cuda()
+    d_pay = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    d_size = torch.zeros(1, dtype=torch.int32, device="cuda")
+    d_out = torch.empty(w * h * 3 // 2, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        codec.compress_device(d_in.data_ptr(), w, h, (50, 50, 50), d_pay.data_ptr(), cap,
+                              d_size.data_ptr(), stream)
+        codec.decompress_device(d_pay.data_ptr(), d_size.data_ptr(), cap, w, h, (50, 50, 50),
+                                d_out.data_ptr(), stream)
+    rc, bad = codec.sync_status(stream)
+    assert rc == 0
+    n = int(d_size.item())
+    assert bytes(d_pay[:n].cpu().numpy()) == g.data
+    assert bytes(d_out.cpu().numpy()) == codec.decompress(g.data, w, h, (50, 50, 50))

@@ -1,0 +1,59 @@
+// codec_common.hpp — shared constants and frame geometry for the gfx950 DCT
+// codec kernels.  Constants restate myyuv_DCT/DCT.cpp:199-230 (quantisation
+// bases, float-literal DCT basis) and Huffman.cpp:32-34 (zig-zag order).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace myyuv_gpu {
+
+constexpr int kWave = 64;
+constexpr int kSlotWords = 40;  // 160-B chunk slot per block (max chunk 155 B)
+constexpr int kMaxChunk = 160;
+
+// Float-literal DCT-II basis, row u = basis u (DCT.cpp:221-230).  Literal
+// values, not cos(): they are slightly asymmetric and bit-exactness depends on
+// them.
+#define MYYUV_DCT_MATRIX                                                                       \
+  {0.3535533845424652f,   0.3535533845424652f,  0.3535533845424652f,  0.3535533845424652f,   \
+   0.3535533845424652f,   0.3535533845424652f,  0.3535533845424652f,  0.3535533845424652f,   \
+   0.4903925955295563f,   0.4157347679138184f,  0.277785062789917f,   0.09754510968923569f,  \
+   -0.09754515439271927f, -0.2777851521968842f, -0.4157347977161407f, -0.4903926253318787f,  \
+   0.4619397222995758f,   0.1913416981697083f,  -0.1913417428731918f, -0.4619397819042206f,  \
+   -0.4619397222995758f,  -0.1913415491580963f, 0.1913417875766754f,  0.4619397521018982f,   \
+   0.4157347679138184f,   -0.09754515439271927f, -0.4903926253318787f, -0.2777849733829498f, \
+   0.2777851819992065f,   0.4903925955295563f,  0.09754502773284912f, -0.4157348573207855f,  \
+   0.3535533547401428f,   -0.3535533547401428f, -0.353553295135498f,  0.3535534739494324f,   \
+   0.3535533547401428f,   -0.3535535931587219f, -0.3535532355308533f, 0.3535533845424652f,   \
+   0.277785062789917f,    -0.4903926253318787f, 0.09754519909620285f, 0.4157346487045288f,   \
+   -0.4157348573207855f,  -0.09754510223865509f, 0.4903926253318787f, -0.2777853906154633f,  \
+   0.1913416981697083f,   -0.4619397222995758f, 0.4619397521018982f,  -0.1913419365882874f,  \
+   -0.1913414746522903f,  0.4619396328926086f,  -0.4619398415088654f, 0.1913419365882874f,   \
+   0.09754510968923569f,  -0.2777849733829498f, 0.4157346487045288f,  -0.4903925657272339f,  \
+   0.4903926849365234f,   -0.4157347679138184f, 0.2777855396270752f,  -0.09754576534032822f}
+
+#define MYYUV_ZIGZAG                                                                          \
+  {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,    \
+   41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,    \
+   30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63}
+
+// Geometry of one IYUV frame as the kernels see it.  Blocks are numbered
+// globally plane-major (Y, U, V), row-major inside a plane, which is the
+// reference's block order k = (y/8)*(w/8) + x/8 per plane (DCT.cpp:308, 355)
+// concatenated over planes.
+struct FrameGeom {
+  uint32_t pw[3], ph[3];  // plane width / height in pixels
+  uint32_t bw[3];         // blocks per block-row
+  uint32_t cum[4];        // cumulative block counts: plane p owns [cum[p], cum[p+1])
+  uint32_t poff[3];       // byte offset of plane p in the IYUV frame
+  uint32_t gpr[3];        // transform groups (8 blocks of one block-row) per block-row
+  uint32_t gcum[4];       // cumulative transform groups
+};
+
+// Tables the kernels read per call (uploaded once per quality triple).
+struct QTables {
+  float q[3][64];     // natural order, DCT.cpp:286-290
+  float qzz[3][64];   // zig-zag order: qzz[p][z] = q[p][zigzag[z]]
+};
+
+}  // namespace myyuv_gpu

@@ -1,0 +1,648 @@
+// myyuv_hip.cpp — implementation of the C ABI in include/myyuv_hip.h.
+//
+// Host side of the gfx950 codec: frame geometry, quantisation tables, the
+// per-context workspace, and the launch sequences
+//   compress:   K1 fdct_quant_zz -> K2 huff_encode -> scan -> K4 compact
+//   decompress: parse -> scan -> K5 huff_decode -> K6 dequant_idct
+// Every launch goes to one stream; nothing synchronises inside the
+// device-resident entry points, so frames pipeline back to back.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "codec_common.hpp"
+#include "k_stream.hpp"
+#include "myyuv_hip.h"
+
+namespace myyuv_gpu {
+__global__ void k_fdct_quant_zz(const uint8_t*, FrameGeom, const QTables*, int16_t*);
+__global__ void k_dequant_idct(const int16_t*, FrameGeom, const QTables*, uint8_t*);
+__global__ void k_huff_encode(const int16_t*, uint32_t, uint32_t*, uint8_t*);
+__global__ void k_scan_tiles(const uint8_t*, ScanSrc, const StreamDesc*, uint32_t*, uint32_t*);
+__global__ void k_scan_sums(uint32_t*, uint32_t, const StreamDesc*);
+__global__ void k_compact(const uint32_t*, const uint8_t*, const uint32_t*, const uint32_t*,
+                          FrameGeom, uint32_t, uint32_t, uint8_t*, uint32_t, uint32_t*,
+                          unsigned long long*);
+__global__ void k_parse(const uint8_t*, const uint32_t*, uint32_t, FrameGeom, StreamDesc*,
+                        unsigned long long*);
+__global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
+                              const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
+                              int16_t*, unsigned long long*);
+extern __constant__ uint8_t c_izigzag[64];
+}  // namespace myyuv_gpu
+
+using namespace myyuv_gpu;
+
+namespace {
+
+constexpr float kLumQ[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
+                             14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
+                             18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
+                             49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+constexpr float kChromaQ[64] = {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+                                24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+                                99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+                                99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+constexpr uint8_t kZigzag[64] = MYYUV_ZIGZAG;
+
+// DCT.cpp:286-290: Q = clamp(roundf(base * mul), 1, 255), mul in float.
+void make_qtable(int q, bool chroma, float out[64]) {
+  const float* base = chroma ? kChromaQ : kLumQ;
+  const float fq = (float)q;
+  const float mul = (fq >= 50.5f) ? (100.0f - fq) / 50.0f : 50.0f / fq;
+  for (int i = 0; i < 64; i++) out[i] = std::min(std::max(std::roundf(base[i] * mul), 1.0f), 255.0f);
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  int grow(size_t want) {
+    if (want <= n) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (hipMalloc(&p, want) != hipSuccess) return MYYUV_E_HIP;
+    n = want;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// Dimension checks in the reference's order: per plane, width then height
+// (applyDCTPlane / restoreDCTPlane, DCT.cpp:280-285, :338-343).
+int make_geom(uint32_t w, uint32_t h, FrameGeom& G) {
+  if (w == 0 || h == 0) return MYYUV_E_WIDTH;
+  if ((uint64_t)w * h * 3 / 2 > 0xFFFFFFFFull) return MYYUV_E_ARG;
+  const uint32_t pw[3] = {w, w / 2, w / 2}, ph[3] = {h, h / 2, h / 2};
+  for (int p = 0; p < 3; p++) {
+    if (pw[p] % 8) return MYYUV_E_WIDTH;
+    if (ph[p] % 8) return MYYUV_E_HEIGHT;
+  }
+  std::memset(&G, 0, sizeof(G));
+  G.cum[0] = 0;
+  G.gcum[0] = 0;
+  for (int p = 0; p < 3; p++) {
+    G.pw[p] = pw[p];
+    G.ph[p] = ph[p];
+    G.bw[p] = pw[p] / 8;
+    G.cum[p + 1] = G.cum[p] + G.bw[p] * (ph[p] / 8);
+    G.gpr[p] = ceil_div(G.bw[p], 8);
+    G.gcum[p + 1] = G.gcum[p] + G.gpr[p] * (ph[p] / 8);
+  }
+  G.poff[0] = 0;
+  G.poff[1] = w * h;
+  G.poff[2] = w * h + (w / 2) * (h / 2);
+  return 0;
+}
+
+}  // namespace
+
+struct myyuv_hip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevBuf frame, coef, slots, sizes, loff, tiles, payload, qt, err, psize, desc;
+  uint8_t q_cached[3] = {0, 0, 0};
+  bool q_valid = false;
+  // profiling
+  bool prof = false;
+  double ms[MYYUV_K_COUNT] = {};
+  int64_t launches[MYYUV_K_COUNT] = {};
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<hipEvent_t> free_events;
+  std::mutex mu;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+hipEvent_t take_event(myyuv_hip_ctx* c) {
+  if (!c->free_events.empty()) {
+    hipEvent_t e = c->free_events.back();
+    c->free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Runs `launch` on `s`, bracketed by events when profiling.
+template <class F>
+int timed(myyuv_hip_ctx* c, int kid, hipStream_t s, F&& launch) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (c->prof) {
+    a = take_event(c);
+    b = take_event(c);
+    (void)hipEventRecord(a, s);
+  }
+  launch();
+  if (hipPeekAtLastError() != hipSuccess) {
+    (void)hipGetLastError();
+    return MYYUV_E_HIP;
+  }
+  if (c->prof) {
+    (void)hipEventRecord(b, s);
+    c->pending.push_back({kid, {a, b}});
+  }
+  return 0;
+}
+
+void drain_profile(myyuv_hip_ctx* c) {
+  for (auto& it : c->pending) {
+    float ms = 0;
+    (void)hipEventSynchronize(it.second.second);
+    if (hipEventElapsedTime(&ms, it.second.first, it.second.second) == hipSuccess) {
+      c->ms[it.first] += ms;
+      c->launches[it.first] += 1;
+    }
+    c->free_events.push_back(it.second.first);
+    c->free_events.push_back(it.second.second);
+  }
+  c->pending.clear();
+}
+
+int upload_qtables(myyuv_hip_ctx* c, const uint8_t q[3], hipStream_t s) {
+  for (int p = 0; p < 3; p++)
+    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  if (c->q_valid && std::memcmp(c->q_cached, q, 3) == 0) return 0;
+  QTables t;
+  for (int p = 0; p < 3; p++) {
+    make_qtable(q[p], p != 0, t.q[p]);
+    for (int z = 0; z < 64; z++) t.qzz[p][z] = t.q[p][kZigzag[z]];
+  }
+  if (c->qt.grow(sizeof(QTables))) return MYYUV_E_HIP;
+  // the table buffer may still be read by queued kernels: order the update
+  // on the stream and wait for it (a quality change is rare).
+  if (hipStreamSynchronize(s) != hipSuccess) return MYYUV_E_HIP;
+  if (hipMemcpy(c->qt.p, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess) return MYYUV_E_HIP;
+  std::memcpy(c->q_cached, q, 3);
+  c->q_valid = true;
+  return 0;
+}
+
+int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
+  const uint32_t nblk = G.cum[3];
+  const uint32_t nwaves = ceil_div(nblk, kWave);
+  const uint32_t ntiles = ceil_div(nblk, kScanTile);
+  int e = 0;
+  e |= c->coef.grow((size_t)nblk * 128);
+  e |= c->slots.grow((size_t)nwaves * kSlotWords * kWave * 4);
+  e |= c->sizes.grow((size_t)nwaves * kWave);
+  e |= c->loff.grow((size_t)nblk * 4);
+  e |= c->tiles.grow((size_t)(ntiles + 1) * 4);
+  e |= c->err.grow(8);
+  e |= c->psize.grow(4);
+  e |= c->desc.grow(sizeof(StreamDesc));
+  return e ? MYYUV_E_HIP : 0;
+}
+
+int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void* d_out,
+                    uint32_t cap, uint32_t* d_size, hipStream_t s) {
+  const uint32_t nblk = G.cum[3];
+  const uint32_t ntiles = ceil_div(nblk, kScanTile);
+  const QTables* qt = c->qt.as<QTables>();
+  unsigned long long* err = c->err.as<unsigned long long>();
+  int e = 0;
+  e |= timed(c, MYYUV_K_FDCT, s, [&] {
+    hipLaunchKernelGGL(k_fdct_quant_zz, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<int16_t>());
+  });
+  e |= timed(c, MYYUV_K_HUFF_ENC, s, [&] {
+    hipLaunchKernelGGL(k_huff_encode, dim3(ceil_div(nblk, kWave)), dim3(kWave), 0, s,
+                       c->coef.as<const int16_t>(), nblk, c->slots.as<uint32_t>(),
+                       c->sizes.as<uint8_t>());
+  });
+  ScanSrc S;
+  for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
+  for (int p = 0; p < 3; p++) S.pos[p] = G.cum[p];
+  e |= timed(c, MYYUV_K_SCAN, s, [&] {
+    hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(256), 0, s, c->sizes.as<const uint8_t>(),
+                       S, (const StreamDesc*)nullptr, c->loff.as<uint32_t>(),
+                       c->tiles.as<uint32_t>());
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, c->tiles.as<uint32_t>(), ntiles,
+                       (const StreamDesc*)nullptr);
+  });
+  const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], 256), t1 = ceil_div(G.cum[2] - G.cum[1], 256),
+                 t2 = ceil_div(G.cum[3] - G.cum[2], 256);
+  e |= timed(c, MYYUV_K_COMPACT, s, [&] {
+    hipLaunchKernelGGL(k_compact, dim3(t0 + t1 + t2), dim3(256), 0, s,
+                       c->slots.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
+                       c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
+                       static_cast<uint8_t*>(d_out), cap, d_size, err);
+  });
+  return e ? MYYUV_E_HIP : 0;
+}
+
+int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
+                      const uint32_t* d_size, uint32_t cap, void* d_out, hipStream_t s) {
+  const uint32_t nblk = G.cum[3];
+  const uint32_t ntiles = ceil_div(nblk, kScanTile);
+  const QTables* qt = c->qt.as<QTables>();
+  unsigned long long* err = c->err.as<unsigned long long>();
+  StreamDesc* desc = c->desc.as<StreamDesc>();
+  const uint8_t* in = static_cast<const uint8_t*>(d_in);
+  int e = 0;
+  e |= timed(c, MYYUV_K_PARSE, s, [&] {
+    hipLaunchKernelGGL(k_parse, dim3(1), dim3(64), 0, s, in, d_size, cap, G, desc, err);
+  });
+  ScanSrc S;
+  for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
+  for (int p = 0; p < 3; p++) S.pos[p] = 0;
+  e |= timed(c, MYYUV_K_SCAN, s, [&] {
+    hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(256), 0, s, in, S,
+                       (const StreamDesc*)desc, c->loff.as<uint32_t>(), c->tiles.as<uint32_t>());
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, c->tiles.as<uint32_t>(), ntiles,
+                       (const StreamDesc*)desc);
+  });
+  const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], kWave),
+                 t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
+                 t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
+  e |= timed(c, MYYUV_K_HUFF_DEC, s, [&] {
+    hipLaunchKernelGGL(k_huff_decode, dim3(t0 + t1 + t2), dim3(kWave), 0, s, in, d_size, cap,
+                       (const StreamDesc*)desc, c->loff.as<const uint32_t>(),
+                       c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<int16_t>(), err);
+  });
+  e |= timed(c, MYYUV_K_IDCT, s, [&] {
+    hipLaunchKernelGGL(k_dequant_idct, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
+                       c->coef.as<const int16_t>(), G, qt, static_cast<uint8_t*>(d_out));
+  });
+  return e ? MYYUV_E_HIP : 0;
+}
+
+int reset_err(myyuv_hip_ctx* c, hipStream_t s) {
+  return hipMemsetAsync(c->err.p, 0xFF, 8, s) == hipSuccess ? 0 : MYYUV_E_HIP;
+}
+
+int read_err(myyuv_hip_ctx* c, hipStream_t s, int64_t* bad_block) {
+  unsigned long long v = ~0ull;
+  if (hipMemcpyAsync(&v, c->err.p, 8, hipMemcpyDeviceToHost, s) != hipSuccess) return MYYUV_E_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return MYYUV_E_HIP;
+  if (bad_block) *bad_block = -1;
+  if (v == ~0ull) return 0;
+  const int code = (int)(v & 0xFF);
+  const uint64_t key = v >> 8;
+  if (bad_block) *bad_block = key == 0 ? -1 : (int64_t)(key >> 1);
+  return code;
+}
+
+// Host mirror of k_parse's header checks (same order), for host buffers.
+int host_parse_headers(const uint8_t* in, uint32_t size) {
+  auto rd32 = [&](uint64_t a) {
+    uint32_t v;
+    std::memcpy(&v, in + a, 4);
+    return v;
+  };
+  if (size <= 12) return MYYUV_E_DCTYUV_SIZE;
+  const uint32_t ps[3] = {rd32(0), rd32(4), rd32(8)};
+  if (12ull + ps[0] + ps[1] + ps[2] > size) return MYYUV_E_DCTYUV_SIZE;
+  uint64_t off = 12;
+  for (int p = 0; p < 3; p++) {
+    if (ps[p] <= 8) return MYYUV_E_PLANE_SIZE;
+    const uint32_t hn = rd32(off), hc = rd32(off + 4);
+    if (hn == 0) return MYYUV_E_PLANE_NBLK;
+    if (hc == 0) return MYYUV_E_PLANE_CONTENT;
+    if (8ull + hn + hc > ps[p]) return MYYUV_E_PLANE_SIZE;
+    off += ps[p];
+  }
+  return 0;
+}
+
+bool hip_ok() {
+  static int ok = -1;
+  if (ok < 0) {
+    int n = 0;
+    ok = (hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : 0;
+  }
+  return ok == 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* myyuv_hip_strerror(int code) {
+  switch (code) {
+    case MYYUV_OK: return "Success";
+    case MYYUV_E_ARG: return "Invalid argument";
+    case MYYUV_E_QUALITY: return "Level of quality must be between 1 and 100";
+    case MYYUV_E_WIDTH: return "Error. width % 8 must be 0";
+    case MYYUV_E_HEIGHT: return "Error. height % 8 must be 0";
+    case MYYUV_E_CAPACITY: return "Output buffer too small for the compressed stream";
+    case MYYUV_E_DCTYUV_SIZE: return "DCTYUV load bad size";
+    case MYYUV_E_PLANE_SIZE: return "DCTYUVPlane load bad size";
+    case MYYUV_E_PLANE_NBLK: return "DCTYUVPlane load chunks_sizes_size bad size";
+    case MYYUV_E_PLANE_CONTENT: return "DCTYUVPlane load content_size bad size";
+    case MYYUV_E_BAD_CODE: return "Huffman bad code";
+    case MYYUV_E_UNKNOWN_SYMBOL: return "Huffman unknown symbol";
+    case MYYUV_E_BAD_CHUNK: return "Huffman bad chunk";
+    case MYYUV_E_HIP: return "HIP runtime error";
+    case MYYUV_E_NO_DEVICE: return "No HIP device available";
+    default: return "Unknown error";
+  }
+}
+
+uint32_t myyuv_dct_payload_bound(uint32_t w, uint32_t h) {
+  const uint64_t nb = (uint64_t)(w / 8) * (h / 8) + 2ull * (uint64_t)(w / 16) * (h / 16);
+  const uint64_t b = 12 + 24 + nb + nb * kMaxChunk;
+  return b > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)((b + 3) & ~3ull);
+}
+
+int myyuv_hip_create(int device, myyuv_hip_handle* out) {
+  if (!out) return MYYUV_E_ARG;
+  *out = nullptr;
+  if (!hip_ok()) return MYYUV_E_NO_DEVICE;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return MYYUV_E_NO_DEVICE;
+  DeviceGuard g(device);
+  auto* c = new myyuv_hip_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return MYYUV_E_HIP;
+  }
+  uint8_t izz[64];
+  for (int z = 0; z < 64; z++) izz[kZigzag[z]] = (uint8_t)z;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(c_izigzag), izz, 64) != hipSuccess ||
+      c->err.grow(8) || c->psize.grow(4) || c->desc.grow(sizeof(StreamDesc)) ||
+      hipMemset(c->err.p, 0xFF, 8) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return MYYUV_E_HIP;
+  }
+  *out = c;
+  return 0;
+}
+
+void myyuv_hip_destroy(myyuv_hip_handle c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  drain_profile(c);
+  for (auto e : c->free_events) (void)hipEventDestroy(e);
+  DevBuf* bufs[] = {&c->frame, &c->coef,    &c->slots, &c->sizes, &c->loff, &c->tiles,
+                    &c->payload, &c->qt,  &c->err,   &c->psize, &c->desc};
+  for (auto* b : bufs) b->release();
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int myyuv_hip_reserve(myyuv_hip_handle c, uint32_t w, uint32_t h) {
+  if (!c) return MYYUV_E_ARG;
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return reserve(c, G);
+}
+
+int myyuv_gpu_dct_compress_device(myyuv_hip_handle c, const void* d_in, uint32_t w, uint32_t h,
+                                  const uint8_t q[3], void* d_out, uint32_t cap,
+                                  uint32_t* d_size, void* stream) {
+  if (!c || !d_in || !d_out || !d_size || !q) return MYYUV_E_ARG;
+  if (((uintptr_t)d_out & 3) || ((uintptr_t)d_in & 7)) return MYYUV_E_ARG;
+  for (int p = 0; p < 3; p++)
+    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  if ((e = reserve(c, G)) || (e = upload_qtables(c, q, s))) return e;
+  return launch_compress(c, G, d_in, d_out, cap, d_size, s);
+}
+
+int myyuv_gpu_dct_decompress_device(myyuv_hip_handle c, const void* d_in, const uint32_t* d_size,
+                                    uint32_t cap, uint32_t w, uint32_t h, const uint8_t q[3],
+                                    void* d_out, void* stream) {
+  if (!c || !d_in || !d_out || !d_size || !q) return MYYUV_E_ARG;
+  if (((uintptr_t)d_in & 3) || ((uintptr_t)d_out & 7)) return MYYUV_E_ARG;
+  for (int p = 0; p < 3; p++)
+    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  if ((e = reserve(c, G)) || (e = upload_qtables(c, q, s))) return e;
+  return launch_decompress(c, G, d_in, d_size, cap, d_out, s);
+}
+
+int myyuv_hip_sync_status(myyuv_hip_handle c, void* stream, int64_t* bad_block) {
+  if (!c) return MYYUV_E_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  int code = read_err(c, s, bad_block);
+  if (reset_err(c, s) || hipStreamSynchronize(s) != hipSuccess) return MYYUV_E_HIP;
+  if (c->prof) drain_profile(c);
+  return code;
+}
+
+int myyuv_gpu_dct_compress(myyuv_hip_handle c, const uint8_t* iyuv, uint32_t w, uint32_t h,
+                           const uint8_t q[3], uint8_t* payload, uint32_t cap,
+                           uint32_t* payload_size) {
+  if (!c || !iyuv || !payload || !payload_size || !q) return MYYUV_E_ARG;
+  for (int p = 0; p < 3; p++)
+    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  const size_t fbytes = (size_t)w * h * 3 / 2;
+  const uint32_t bound = myyuv_dct_payload_bound(w, h);
+  if ((e = reserve(c, G)) || (e = upload_qtables(c, q, s))) return e;
+  if (c->frame.grow(fbytes) || c->payload.grow(bound)) return MYYUV_E_HIP;
+  if (reset_err(c, s)) return MYYUV_E_HIP;
+  if (hipMemcpyAsync(c->frame.p, iyuv, fbytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return MYYUV_E_HIP;
+  if ((e = launch_compress(c, G, c->frame.p, c->payload.p, bound, c->psize.as<uint32_t>(), s)))
+    return e;
+  uint32_t size = 0;
+  if (hipMemcpyAsync(&size, c->psize.p, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return MYYUV_E_HIP;
+  int64_t bad = -1;
+  if ((e = read_err(c, s, &bad))) {
+    (void)reset_err(c, s);
+    return e;
+  }
+  *payload_size = size;
+  if (size > cap) return MYYUV_E_CAPACITY;
+  if (hipMemcpyAsync(payload, c->payload.p, size, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return MYYUV_E_HIP;
+  if (c->prof) drain_profile(c);
+  return 0;
+}
+
+int myyuv_gpu_dct_decompress(myyuv_hip_handle c, const uint8_t* payload, uint32_t size, uint32_t w,
+                             uint32_t h, const uint8_t q[3], uint8_t* iyuv, int64_t* bad_block) {
+  if (bad_block) *bad_block = -1;
+  if (!c || !payload || !iyuv || !q) return MYYUV_E_ARG;
+  int e_hdr = 0;
+  for (int p = 0; p < 3; p++)
+    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  // DCTYUV::load / DCTYUVPlane::load checks (DCT.cpp:454 -> :130-159, :39-62)
+  // come before the dimension checks in the reference: validate the stream
+  // header on the host (the device re-checks it in k_parse).
+  if ((e_hdr = host_parse_headers(payload, size))) return e_hdr;
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  const uint32_t cap = (size + 3) & ~3u;
+  const size_t fbytes = (size_t)w * h * 3 / 2;
+  if ((e = reserve(c, G)) || (e = upload_qtables(c, q, s))) return e;
+  if (c->frame.grow(fbytes) || c->payload.grow(cap)) return MYYUV_E_HIP;
+  if (reset_err(c, s)) return MYYUV_E_HIP;
+  if (hipMemsetAsync(static_cast<uint8_t*>(c->payload.p) + (cap - 4), 0, 4, s) != hipSuccess ||
+      hipMemcpyAsync(c->payload.p, payload, size, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(c->psize.p, &size, 4, hipMemcpyHostToDevice, s) != hipSuccess)
+    return MYYUV_E_HIP;
+  if ((e = launch_decompress(c, G, c->payload.p, c->psize.as<const uint32_t>(), cap, c->frame.p, s)))
+    return e;
+  if ((e = read_err(c, s, bad_block))) {
+    (void)reset_err(c, s);
+    (void)hipStreamSynchronize(s);
+    return e;
+  }
+  if (hipMemcpyAsync(iyuv, c->frame.p, fbytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return MYYUV_E_HIP;
+  if (c->prof) drain_profile(c);
+  return 0;
+}
+
+int myyuv_hip_profile(myyuv_hip_handle c, int enable) {
+  if (!c) return MYYUV_E_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  drain_profile(c);
+  c->prof = enable != 0;
+  for (int k = 0; k < MYYUV_K_COUNT; k++) {
+    c->ms[k] = 0;
+    c->launches[k] = 0;
+  }
+  return 0;
+}
+
+int myyuv_hip_kernel_stats(myyuv_hip_handle c, double ms[MYYUV_K_COUNT],
+                           int64_t launches[MYYUV_K_COUNT]) {
+  if (!c || !ms || !launches) return MYYUV_E_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  drain_profile(c);
+  for (int k = 0; k < MYYUV_K_COUNT; k++) {
+    ms[k] = c->ms[k];
+    launches[k] = c->launches[k];
+  }
+  return 0;
+}
+
+// ---- block-level KAT entry points -----------------------------------------
+int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblocks,
+                          const float qtable[64], int16_t* coef_zz) {
+  if (!c || !px || !qtable || !coef_zz || nblocks == 0) return MYYUV_E_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  // one plane of width 8 (one block per block-row); planes 1, 2 empty
+  FrameGeom G;
+  std::memset(&G, 0, sizeof(G));
+  G.pw[0] = 8;
+  G.ph[0] = 8 * nblocks;
+  G.bw[0] = 1;
+  G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
+  G.gpr[0] = 1;
+  G.gcum[1] = G.gcum[2] = G.gcum[3] = nblocks;
+  QTables t;
+  std::memset(&t, 0, sizeof(t));
+  std::memcpy(t.q[0], qtable, 256);
+  if (reserve(c, G) || c->frame.grow((size_t)nblocks * 64) || c->qt.grow(sizeof(QTables)))
+    return MYYUV_E_HIP;
+  c->q_valid = false;
+  if (hipStreamSynchronize(s) != hipSuccess ||
+      hipMemcpy(c->qt.p, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->frame.p, px, (size_t)nblocks * 64, hipMemcpyHostToDevice) != hipSuccess)
+    return MYYUV_E_HIP;
+  hipLaunchKernelGGL(k_fdct_quant_zz, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
+                     c->frame.as<const uint8_t>(), G, c->qt.as<const QTables>(),
+                     c->coef.as<int16_t>());
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(coef_zz, c->coef.p, (size_t)nblocks * 128, hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return MYYUV_E_HIP;
+  return 0;
+}
+
+int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uint32_t nblocks,
+                                 uint8_t* chunks160, uint8_t* sizes) {
+  if (!c || !coef_zz || !chunks160 || !sizes || nblocks == 0) return MYYUV_E_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  FrameGeom G;
+  std::memset(&G, 0, sizeof(G));
+  G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
+  if (reserve(c, G)) return MYYUV_E_HIP;
+  const uint32_t nwaves = ceil_div(nblocks, kWave);
+  if (hipMemcpy(c->coef.p, coef_zz, (size_t)nblocks * 128, hipMemcpyHostToDevice) != hipSuccess)
+    return MYYUV_E_HIP;
+  hipLaunchKernelGGL(k_huff_encode, dim3(nwaves), dim3(kWave), 0, s, c->coef.as<const int16_t>(),
+                     nblocks, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>());
+  std::vector<uint32_t> slots((size_t)nwaves * kSlotWords * kWave);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(slots.data(), c->slots.p, slots.size() * 4, hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipMemcpyAsync(sizes, c->sizes.p, nblocks, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return MYYUV_E_HIP;
+  for (uint32_t b = 0; b < nblocks; b++) {
+    const uint32_t* base = slots.data() + (size_t)(b / kWave) * kSlotWords * kWave + (b % kWave);
+    uint8_t* dst = chunks160 + (size_t)b * kMaxChunk;
+    std::memset(dst, 0, kMaxChunk);
+    const uint32_t nw = (sizes[b] + 3u) / 4u;
+    for (uint32_t j = 0; j < nw && j < (uint32_t)kSlotWords; j++) {
+      const uint32_t v = base[(size_t)j * kWave];
+      std::memcpy(dst + 4 * j, &v, 4);
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,218 @@
+"""ctypes binding of the C ABI (include/myyuv_hip.h) of the gfx950 DCT codec.
+
+This is the Python view of the product path: every call goes to
+libmyyuv_hip.so (HIP kernels).  There is no CPU fallback — if the library or
+a GPU is missing, calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmyyuv_hip.so")
+
+OK = 0
+E_ARG, E_QUALITY, E_WIDTH, E_HEIGHT, E_CAPACITY = 1, 2, 3, 4, 5
+E_DCTYUV_SIZE, E_PLANE_SIZE, E_PLANE_NBLK, E_PLANE_CONTENT = 6, 7, 8, 9
+E_BAD_CODE, E_UNKNOWN_SYMBOL, E_BAD_CHUNK, E_HIP, E_NO_DEVICE = 10, 11, 12, 13, 14
+
+KERNELS = ["fdct_quant_zz", "huff_encode", "scan", "compact", "parse", "huff_decode",
+           "dequant_idct"]
+K_FDCT, K_HUFF_ENC, K_SCAN, K_COMPACT, K_PARSE, K_HUFF_DEC, K_IDCT = range(7)
+
+# the exported symbols include/myyuv_hip.h declares (checked by the CPU tests)
+EXPORTS = [
+    "myyuv_hip_create", "myyuv_hip_destroy", "myyuv_hip_strerror", "myyuv_dct_payload_bound",
+    "myyuv_gpu_dct_compress", "myyuv_gpu_dct_decompress", "myyuv_hip_reserve",
+    "myyuv_gpu_dct_compress_device", "myyuv_gpu_dct_decompress_device", "myyuv_hip_sync_status",
+    "myyuv_hip_profile", "myyuv_hip_kernel_stats", "myyuv_gpu_fdct_blocks",
+    "myyuv_gpu_huff_encode_blocks",
+]
+
+_lib = None
+
+
+class CodecError(RuntimeError):
+    """A MYYUV_E_* failure; .code is the number, str() the reference's message."""
+
+    def __init__(self, code, bad_block=-1):
+        self.code = code
+        self.bad_block = bad_block
+        super().__init__(strerror(code) if _lib is not None else f"error {code}")
+
+
+def _share_hip_runtime_with_torch():
+    """torch ships its own libamdhip64 with the same soname (libamdhip64.so.7)
+    as /opt/rocm's.  Two copies in one process means two HIP/HSA runtimes and
+    the second one finds no GPU.  When torch is importable, load it first so
+    this library binds to the runtime torch already mapped (the loader matches
+    our NEEDED libamdhip64.so.7 against it); without torch the library uses
+    /opt/rocm's runtime through its RUNPATH."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if os.environ.get("MYYUV_NO_TORCH_RUNTIME") != "1":
+        _share_hip_runtime_with_torch()
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} missing: build it with `make -C yuv-manipulations-2_amd`"
+                                " or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    vp = ctypes.c_void_p
+    u32 = ctypes.c_uint32
+    L.myyuv_hip_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.myyuv_hip_destroy.argtypes = [vp]
+    L.myyuv_hip_destroy.restype = None
+    L.myyuv_hip_strerror.argtypes = [ctypes.c_int]
+    L.myyuv_hip_strerror.restype = ctypes.c_char_p
+    L.myyuv_dct_payload_bound.argtypes = [u32, u32]
+    L.myyuv_dct_payload_bound.restype = u32
+    L.myyuv_gpu_dct_compress.argtypes = [vp, u8p, u32, u32, u8p, u8p, u32, ctypes.POINTER(u32)]
+    L.myyuv_gpu_dct_decompress.argtypes = [vp, u8p, u32, u32, u32, u8p, u8p,
+                                           ctypes.POINTER(ctypes.c_int64)]
+    L.myyuv_hip_reserve.argtypes = [vp, u32, u32]
+    L.myyuv_gpu_dct_compress_device.argtypes = [vp, vp, u32, u32, u8p, vp, u32, vp, vp]
+    L.myyuv_gpu_dct_decompress_device.argtypes = [vp, vp, vp, u32, u32, u32, u8p, vp, vp]
+    L.myyuv_hip_sync_status.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int64)]
+    L.myyuv_hip_profile.argtypes = [vp, ctypes.c_int]
+    L.myyuv_hip_kernel_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_int64)]
+    L.myyuv_gpu_fdct_blocks.argtypes = [vp, u8p, u32, ctypes.POINTER(ctypes.c_float),
+                                        ctypes.POINTER(ctypes.c_int16)]
+    L.myyuv_gpu_huff_encode_blocks.argtypes = [vp, ctypes.POINTER(ctypes.c_int16), u32, u8p, u8p]
+    _lib = L
+    return L
+
+
+def strerror(code):
+    return load().myyuv_hip_strerror(int(code)).decode()
+
+
+def payload_bound(w, h):
+    return load().myyuv_dct_payload_bound(w, h)
+
+
+def _u8(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def _q(q):
+    return np.ascontiguousarray(np.array(q, dtype=np.int64).astype(np.uint8))
+
+
+class Codec:
+    """One context (HIP stream + workspace) on one device."""
+
+    def __init__(self, device=0):
+        L = load()
+        h = ctypes.c_void_p()
+        rc = L.myyuv_hip_create(int(device), ctypes.byref(h))
+        if rc:
+            raise CodecError(rc)
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if self._h:
+            load().myyuv_hip_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host-buffer API (what YUV::compress_map / decompress_map call) --
+    def compress(self, iyuv, w, h, q):
+        """IYUV bytes -> DCTYUV payload bytes."""
+        src = np.ascontiguousarray(np.frombuffer(memoryview(iyuv).cast("B"), np.uint8))
+        if src.size < w * h * 3 // 2:
+            raise ValueError("frame smaller than W*H*3/2")
+        qa = _q(q)
+        cap = payload_bound(w, h)
+        out = np.empty(cap, np.uint8)
+        size = ctypes.c_uint32(0)
+        rc = load().myyuv_gpu_dct_compress(self._h, _u8(src), w, h, _u8(qa), _u8(out), cap,
+                                           ctypes.byref(size))
+        if rc:
+            raise CodecError(rc)
+        return out[: size.value].tobytes()
+
+    def decompress(self, payload, w, h, q):
+        src = np.ascontiguousarray(np.frombuffer(memoryview(payload).cast("B"), np.uint8))
+        qa = _q(q)
+        out = np.empty(w * h * 3 // 2, np.uint8)
+        bad = ctypes.c_int64(-1)
+        rc = load().myyuv_gpu_dct_decompress(self._h, _u8(src), src.size, w, h, _u8(qa),
+                                             _u8(out), ctypes.byref(bad))
+        if rc:
+            raise CodecError(rc, bad.value)
+        return out.tobytes()
+
+    # -- device-resident API (pointers are device addresses, e.g. torch data_ptr) --
+    def reserve(self, w, h):
+        rc = load().myyuv_hip_reserve(self._h, w, h)
+        if rc:
+            raise CodecError(rc)
+
+    def compress_device(self, d_iyuv, w, h, q, d_payload, cap, d_size, stream=None):
+        rc = load().myyuv_gpu_dct_compress_device(self._h, d_iyuv, w, h, _u8(_q(q)), d_payload,
+                                                  cap, d_size, stream)
+        if rc:
+            raise CodecError(rc)
+
+    def decompress_device(self, d_payload, d_size, cap, w, h, q, d_iyuv, stream=None):
+        rc = load().myyuv_gpu_dct_decompress_device(self._h, d_payload, d_size, cap, w, h,
+                                                    _u8(_q(q)), d_iyuv, stream)
+        if rc:
+            raise CodecError(rc)
+
+    def sync_status(self, stream=None):
+        bad = ctypes.c_int64(-1)
+        rc = load().myyuv_hip_sync_status(self._h, stream, ctypes.byref(bad))
+        return rc, bad.value
+
+    def profile(self, enable):
+        rc = load().myyuv_hip_profile(self._h, 1 if enable else 0)
+        if rc:
+            raise CodecError(rc)
+
+    def kernel_stats(self):
+        ms = (ctypes.c_double * 7)()
+        n = (ctypes.c_int64 * 7)()
+        rc = load().myyuv_hip_kernel_stats(self._h, ms, n)
+        if rc:
+            raise CodecError(rc)
+        return {KERNELS[i]: (ms[i], n[i]) for i in range(7)}
+
+    # -- block-level known-answer entry points --
+    def fdct_blocks(self, px, qtable):
+        px = np.ascontiguousarray(px, np.uint8).reshape(-1, 64)
+        qt = np.ascontiguousarray(qtable, np.float32).reshape(64)
+        out = np.empty((px.shape[0], 64), np.int16)
+        rc = load().myyuv_gpu_fdct_blocks(self._h, _u8(px), px.shape[0],
+                                          qt.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                          out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)))
+        if rc:
+            raise CodecError(rc)
+        return out
+
+    def huff_encode_blocks(self, coef_zz):
+        c = np.ascontiguousarray(coef_zz, np.int16).reshape(-1, 64)
+        n = c.shape[0]
+        chunks = np.zeros((n, 160), np.uint8)
+        sizes = np.zeros(n, np.uint8)
+        rc = load().myyuv_gpu_huff_encode_blocks(
+            self._h, c.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)), n, _u8(chunks), _u8(sizes))
+        if rc:
+            raise CodecError(rc)
+        return [chunks[i, : sizes[i]].tobytes() for i in range(n)]
