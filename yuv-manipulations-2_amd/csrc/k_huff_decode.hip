@@ -18,7 +18,7 @@
 //      (uint8 arithmetic of `first` kept), and the bit budget checks give the
 //      same "bad code" / "unknown symbol" outcomes.
 // Output: 64 int16 per block in zig-zag order (decode order), zero-filled
-// after the last symbol, written coalesced through a padded LDS transpose.
+// after the last symbol, in the block-interleaved layout of K1/K6.
 #include "codec_common.hpp"
 #include "k_stream.hpp"
 
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(64) void k_huff_decode(const uint8_t* __restrict__ 
                                                    const uint32_t* __restrict__ tile_pre,
                                                    FrameGeom G, uint32_t tiles_p0,
                                                    uint32_t tiles_p1,
-                                                   int16_t* __restrict__ coef,
+                                                   uint32_t* __restrict__ coefw,
                                                    unsigned long long* __restrict__ err) {
   __shared__ uint32_t stage[kStageWords];
   __shared__ uint32_t symw[32 * kWave];
@@ -230,13 +230,12 @@ __global__ __launch_bounds__(64) void k_huff_decode(const uint8_t* __restrict__ 
   }
   __syncthreads();
 
-  // ---- coalesced write-out: word w of block l -> coef[(g0+l)*64 + 2w, +1]
-  uint32_t* dst = reinterpret_cast<uint32_t*>(coef);
-#pragma unroll 4
-  for (int r = 0; r < 32; r++) {
-    const int idx = r * kWave + lane;
-    const int l = idx >> 5, w = idx & 31;
-    if (g0 + l < g1) dst[(size_t)(g0 + l) * 32 + w] = outw[w * kOutStride + l];
+  // ---- write-out in the block-interleaved layout K6 reads: word w of block
+  // g at ((g>>6)*32 + w)*64 + (g&63) (256 contiguous bytes per store).
+  if (live) {
+    uint32_t* dst = coefw + (size_t)(g >> 6) * 32 * 64 + (g & 63);
+#pragma unroll 8
+    for (int w = 0; w < 32; w++) dst[w * 64] = outw[w * kOutStride + lane];
   }
 }
 

@@ -56,13 +56,14 @@ __device__ __forceinline__ GroupPos locate_group(const FrameGeom& G, uint32_t gr
 
 }  // namespace
 
-// K1: u8 planes -> int16 coefficients, zig-zag order, [block][64].
+// K1: u8 planes -> int16 coefficients, zig-zag order, block-interleaved words.
 // DCT.cpp:297-306 (gather, -128), :269-277 (applyDCTBlock), Huffman.cpp:176-182
 // (zig-zag gather).
 __global__ __launch_bounds__(256) void k_fdct_quant_zz(const uint8_t* __restrict__ frame,
                                                       FrameGeom G,
                                                       const QTables* __restrict__ qt,
-                                                      int16_t* __restrict__ coef) {
+                                                      uint32_t* __restrict__ coefw,
+                                                      uint8_t* __restrict__ mszs) {
   __shared__ float tile_all[4][kGroupBlocks * kTileStride];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -149,18 +150,37 @@ __global__ __launch_bounds__(256) void k_fdct_quant_zz(const uint8_t* __restrict
   }
   wave_sync();
 
-  // ---- store: lane (s=r, b) writes zig-zag coefficients s*8..s*8+7 (16 B).
-  if (live) {
+  // ---- store: lane (s=r, b) writes zig-zag words 4s..4s+3 of block b into
+  // the block-interleaved layout K2 reads (word w of block g at
+  // ((g>>6)*32 + w)*64 + (g&63)), and the message length msz (1 + index of
+  // the last nonzero zig-zag coefficient, Huffman.cpp:176-190) per block.
+  {
     const uint4 v = *reinterpret_cast<const uint4*>(
         reinterpret_cast<const int16_t*>(tile + b * kTileStride) + r * 8);
-    *reinterpret_cast<uint4*>(coef + (size_t)(gp.g0 + b) * 64 + r * 8) = v;
+    const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
+    int last = -1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (w8[k] & 0xFFFFu) last = r * 8 + 2 * k;
+      if (w8[k] >> 16) last = r * 8 + 2 * k + 1;
+    }
+    last = max(last, __shfl_xor(last, 8, 64));
+    last = max(last, __shfl_xor(last, 16, 64));
+    last = max(last, __shfl_xor(last, 32, 64));
+    if (live) {
+      const uint32_t g = gp.g0 + b;
+      uint32_t* dst = coefw + (size_t)(g >> 6) * 32 * 64 + (g & 63);
+#pragma unroll
+      for (int k = 0; k < 4; k++) dst[(r * 4 + k) * 64] = w8[k];
+      if (r == 0) mszs[g] = (uint8_t)(last + 1);
+    }
   }
 }
 
-// K6: int16 zig-zag coefficients [block][64] -> u8 planes.
+// K6: int16 zig-zag coefficients (block-interleaved words) -> u8 planes.
 // DCT.cpp:330-334 (dequant, squareMatrixMulT2, squareMatrixMul), :358-362
 // (roundf, +128, clamp).
-__global__ __launch_bounds__(256) void k_dequant_idct(const int16_t* __restrict__ coef,
+__global__ __launch_bounds__(256) void k_dequant_idct(const uint32_t* __restrict__ coefw,
                                                      FrameGeom G,
                                                      const QTables* __restrict__ qt,
                                                      uint8_t* __restrict__ frame) {
@@ -178,7 +198,11 @@ __global__ __launch_bounds__(256) void k_dequant_idct(const int16_t* __restrict_
   // scatter them to their natural positions in the tile.
   {
     uint4 raw = make_uint4(0, 0, 0, 0);
-    if (live) raw = *reinterpret_cast<const uint4*>(coef + (size_t)(gp.g0 + b) * 64 + r * 8);
+    if (live) {
+      const uint32_t g = gp.g0 + b;
+      const uint32_t* src = coefw + (size_t)(g >> 6) * 32 * 64 + (g & 63) + (r * 4) * 64;
+      raw = make_uint4(src[0], src[64], src[128], src[192]);
+    }
     const uint2 zz = *reinterpret_cast<const uint2*>(&c_zigzag[r * 8]);
     const float4* qrow = reinterpret_cast<const float4*>(&qt->qzz[gp.p][r * 8]);
     const float4 q0 = qrow[0], q1 = qrow[1];

@@ -20,9 +20,12 @@
 #include "myyuv_hip.h"
 
 namespace myyuv_gpu {
-__global__ void k_fdct_quant_zz(const uint8_t*, FrameGeom, const QTables*, int16_t*);
-__global__ void k_dequant_idct(const int16_t*, FrameGeom, const QTables*, uint8_t*);
-__global__ void k_huff_encode(const int16_t*, uint32_t, uint32_t*, uint8_t*);
+__global__ void k_fdct_quant_zz(const uint8_t*, FrameGeom, const QTables*, uint32_t*, uint8_t*);
+__global__ void k_dequant_idct(const uint32_t*, FrameGeom, const QTables*, uint8_t*);
+__global__ void k_huff_encode(const uint32_t*, const uint8_t*, uint32_t, uint32_t*, uint8_t*,
+                              uint32_t*, uint32_t*);
+__global__ void k_huff_encode_wide(const uint32_t*, const uint8_t*, uint32_t*, uint8_t*,
+                                   const uint32_t*, const uint32_t*);
 __global__ void k_scan_tiles(const uint8_t*, ScanSrc, const StreamDesc*, uint32_t*, uint32_t*);
 __global__ void k_scan_sums(uint32_t*, uint32_t, const StreamDesc*);
 __global__ void k_compact(const uint32_t*, const uint8_t*, const uint32_t*, const uint32_t*,
@@ -32,8 +35,11 @@ __global__ void k_parse(const uint8_t*, const uint32_t*, uint32_t, FrameGeom, St
                         unsigned long long*);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
-                              int16_t*, unsigned long long*);
+                              uint32_t*, unsigned long long*);
 extern __constant__ uint8_t c_izigzag[64];
+#ifdef MYYUV_STAMPS
+extern __device__ unsigned long long g_k2_stamps[8];
+#endif
 }  // namespace myyuv_gpu
 
 using namespace myyuv_gpu;
@@ -115,7 +121,7 @@ int make_geom(uint32_t w, uint32_t h, FrameGeom& G) {
 struct myyuv_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf frame, coef, slots, sizes, loff, tiles, payload, qt, err, psize, desc;
+  DevBuf frame, coef, msz, slots, sizes, loff, tiles, payload, qt, err, psize, desc, work;
   uint8_t q_cached[3] = {0, 0, 0};
   bool q_valid = false;
   // profiling
@@ -211,7 +217,8 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   const uint32_t nwaves = ceil_div(nblk, kWave);
   const uint32_t ntiles = ceil_div(nblk, kScanTile);
   int e = 0;
-  e |= c->coef.grow((size_t)nblk * 128);
+  e |= c->coef.grow((size_t)nwaves * 32 * kWave * 4);  // block-interleaved words
+  e |= c->msz.grow((size_t)nwaves * kWave);
   e |= c->slots.grow((size_t)nwaves * kSlotWords * kWave * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
   e |= c->loff.grow((size_t)nblk * 4);
@@ -219,7 +226,25 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->err.grow(8);
   e |= c->psize.grow(4);
   e |= c->desc.grow(sizeof(StreamDesc));
+  e |= c->work.grow((size_t)nblk * 4 + 256);  // [0]: overflow count, then block ids
   return e ? MYYUV_E_HIP : 0;
+}
+
+// K2: fast pass over all blocks, then the wide pass over the blocks with more
+// than 16 distinct symbols (worklist filled on the device; no host sync).
+int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, hipStream_t s) {
+  uint32_t* count = c->work.as<uint32_t>();
+  uint32_t* list = count + 64;
+  if (hipMemsetAsync(count, 0, 4, s) != hipSuccess) return MYYUV_E_HIP;
+  return timed(c, MYYUV_K_HUFF_ENC, s, [&] {
+    hipLaunchKernelGGL(k_huff_encode, dim3(ceil_div(nblk, kWave)), dim3(kWave), 0, s,
+                       c->coef.as<const uint32_t>(), c->msz.as<const uint8_t>(), nblk,
+                       c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(), list, count);
+    hipLaunchKernelGGL(k_huff_encode_wide, dim3(ceil_div(nblk, kWave)), dim3(kWave), 0, s,
+                       c->coef.as<const uint32_t>(), c->msz.as<const uint8_t>(),
+                       c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(), (const uint32_t*)list,
+                       (const uint32_t*)count);
+  });
 }
 
 int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void* d_out,
@@ -231,13 +256,10 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   int e = 0;
   e |= timed(c, MYYUV_K_FDCT, s, [&] {
     hipLaunchKernelGGL(k_fdct_quant_zz, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
-                       static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<int16_t>());
+                       static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint32_t>(),
+                       c->msz.as<uint8_t>());
   });
-  e |= timed(c, MYYUV_K_HUFF_ENC, s, [&] {
-    hipLaunchKernelGGL(k_huff_encode, dim3(ceil_div(nblk, kWave)), dim3(kWave), 0, s,
-                       c->coef.as<const int16_t>(), nblk, c->slots.as<uint32_t>(),
-                       c->sizes.as<uint8_t>());
-  });
+  e |= launch_huff_encode(c, nblk, s);
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
   for (int p = 0; p < 3; p++) S.pos[p] = G.cum[p];
@@ -286,11 +308,11 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
   e |= timed(c, MYYUV_K_HUFF_DEC, s, [&] {
     hipLaunchKernelGGL(k_huff_decode, dim3(t0 + t1 + t2), dim3(kWave), 0, s, in, d_size, cap,
                        (const StreamDesc*)desc, c->loff.as<const uint32_t>(),
-                       c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<int16_t>(), err);
+                       c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<uint32_t>(), err);
   });
   e |= timed(c, MYYUV_K_IDCT, s, [&] {
     hipLaunchKernelGGL(k_dequant_idct, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
-                       c->coef.as<const int16_t>(), G, qt, static_cast<uint8_t*>(d_out));
+                       c->coef.as<const uint32_t>(), G, qt, static_cast<uint8_t*>(d_out));
   });
   return e ? MYYUV_E_HIP : 0;
 }
@@ -405,8 +427,8 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   (void)hipStreamSynchronize(c->stream);
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
-  DevBuf* bufs[] = {&c->frame, &c->coef,    &c->slots, &c->sizes, &c->loff, &c->tiles,
-                    &c->payload, &c->qt,  &c->err,   &c->psize, &c->desc};
+  DevBuf* bufs[] = {&c->frame, &c->coef, &c->msz,    &c->slots, &c->sizes, &c->loff, &c->tiles,
+                    &c->payload, &c->qt,  &c->err,   &c->psize, &c->desc, &c->work};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -573,6 +595,20 @@ int myyuv_hip_kernel_stats(myyuv_hip_handle c, double ms[MYYUV_K_COUNT],
   return 0;
 }
 
+// Diagnostic builds (-DMYYUV_STAMPS): summed per-stage wave cycles of K2
+// since the last call; returns MYYUV_E_ARG in normal builds.
+int myyuv_debug_k2_stamps(unsigned long long out[8]) {
+#ifdef MYYUV_STAMPS
+  unsigned long long zero[8] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_stamps), 64) != hipSuccess) return MYYUV_E_HIP;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_k2_stamps), zero, 64) != hipSuccess) return MYYUV_E_HIP;
+  return 0;
+#else
+  (void)out;
+  return MYYUV_E_ARG;
+#endif
+}
+
 // ---- block-level KAT entry points -----------------------------------------
 int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblocks,
                           const float qtable[64], int16_t* coef_zz) {
@@ -601,12 +637,17 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
     return MYYUV_E_HIP;
   hipLaunchKernelGGL(k_fdct_quant_zz, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
                      c->frame.as<const uint8_t>(), G, c->qt.as<const QTables>(),
-                     c->coef.as<int16_t>());
+                     c->coef.as<uint32_t>(), c->msz.as<uint8_t>());
+  std::vector<uint32_t> words((size_t)ceil_div(nblocks, kWave) * 32 * kWave);
   if (hipGetLastError() != hipSuccess ||
-      hipMemcpyAsync(coef_zz, c->coef.p, (size_t)nblocks * 128, hipMemcpyDeviceToHost, s) !=
+      hipMemcpyAsync(words.data(), c->coef.p, words.size() * 4, hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return MYYUV_E_HIP;
+  for (uint32_t g = 0; g < nblocks; g++)
+    for (int w = 0; w < 32; w++)
+      std::memcpy(coef_zz + (size_t)g * 64 + 2 * w,
+                  &words[((size_t)(g >> 6) * 32 + w) * kWave + (g & 63)], 4);
   return 0;
 }
 
@@ -621,13 +662,24 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
   if (reserve(c, G)) return MYYUV_E_HIP;
   const uint32_t nwaves = ceil_div(nblocks, kWave);
-  if (hipMemcpy(c->coef.p, coef_zz, (size_t)nblocks * 128, hipMemcpyHostToDevice) != hipSuccess)
+  // host-side relayout into K1's output format: block-interleaved words + msz
+  std::vector<uint32_t> words((size_t)nwaves * 32 * kWave, 0u);
+  std::vector<uint8_t> msz((size_t)nwaves * kWave, 0);
+  for (uint32_t g = 0; g < nblocks; g++) {
+    const int16_t* src = coef_zz + (size_t)g * 64;
+    int last = -1;
+    for (int i = 0; i < 64; i++)
+      if (src[i] != 0) last = i;
+    msz[g] = (uint8_t)(last + 1);
+    for (int w = 0; w < 32; w++)
+      std::memcpy(&words[((size_t)(g >> 6) * 32 + w) * kWave + (g & 63)], src + 2 * w, 4);
+  }
+  if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->msz.p, msz.data(), msz.size(), hipMemcpyHostToDevice) != hipSuccess)
     return MYYUV_E_HIP;
-  hipLaunchKernelGGL(k_huff_encode, dim3(nwaves), dim3(kWave), 0, s, c->coef.as<const int16_t>(),
-                     nblocks, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>());
+  if (launch_huff_encode(c, nblocks, s)) return MYYUV_E_HIP;
   std::vector<uint32_t> slots((size_t)nwaves * kSlotWords * kWave);
-  if (hipGetLastError() != hipSuccess ||
-      hipMemcpyAsync(slots.data(), c->slots.p, slots.size() * 4, hipMemcpyDeviceToHost, s) !=
+  if (hipMemcpyAsync(slots.data(), c->slots.p, slots.size() * 4, hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
       hipMemcpyAsync(sizes, c->sizes.p, nblocks, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmyyuv_hip.so")
+# MYYUV_HIP_LIB selects a diagnostic build (e.g. build/stamps/libmyyuv_hip.so)
+LIB_PATH = os.environ.get("MYYUV_HIP_LIB") or os.path.join(_HERE, "libmyyuv_hip.so")
 
 OK = 0
 E_ARG, E_QUALITY, E_WIDTH, E_HEIGHT, E_CAPACITY = 1, 2, 3, 4, 5
