@@ -183,7 +183,12 @@ def main():
         step(i % nslot)
     gathered = None
     if world > 1:
-        gathered = gather_streams(dist, d_pay, d_size, args.steps, world, rank, dev)
+        # the batch's exchange step: every rank's compressed streams to rank 0
+        import batch
+        nframes = world * args.steps
+        got = batch.gather_streams(dist, [d_pay[i % nslot] for i in range(args.steps)],
+                                   d_size[:args.steps], nframes, world, rank, dev)
+        gathered = len(got) if got is not None else 0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -236,30 +241,6 @@ def main():
     codec.close()
     if world > 1:
         dist.destroy_process_group()
-
-
-def gather_streams(dist, d_pay, d_size, steps, world, rank, dev):
-    """RCCL gather of every rank's compressed streams to rank 0: all-gather the
-    u32 sizes, then exact-size point-to-point sends (batched in one group)."""
-    import torch
-    sizes = torch.empty((world, steps), dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(sizes, d_size[:steps].contiguous())
-    hs = sizes.cpu().tolist()
-    ops = []
-    recv = []
-    if rank == 0:
-        for r in range(1, world):
-            for i in range(steps):
-                buf = torch.empty(hs[r][i], dtype=torch.uint8, device=dev)
-                recv.append(buf)
-                ops.append(dist.P2POp(dist.irecv, buf, r))
-    else:
-        for i in range(steps):
-            ops.append(dist.P2POp(dist.isend, d_pay[i, :hs[rank][i]], 0))
-    if ops:
-        for rq in dist.batch_isend_irecv(ops):
-            rq.wait()
-    return world * steps if rank == 0 else 0
 
 
 if __name__ == "__main__":

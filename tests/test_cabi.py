@@ -1,0 +1,83 @@
+"""The C-ABI library (the drop-in boundary) loads and exports every entry point
+include/myyuv_hip.h declares; host-side logic that needs no GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import PKG, ROOT
+
+HEADER = os.path.join(ROOT, "include", "myyuv_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\*?(myyuv_[a-z_0-9]+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    assert "myyuv_gpu_dct_compress" in names and "myyuv_gpu_dct_decompress" in names
+    assert len(names) >= 14
+
+
+def test_library_exports_every_declared_symbol():
+    import myyuv_hip
+    lib = ctypes.CDLL(myyuv_hip.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert sorted(myyuv_hip.EXPORTS) == sorted(declared_functions())
+
+
+def test_exported_symbols_are_plain_c():
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(PKG, "libmyyuv_hip.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    for name in declared_functions():
+        assert name in exported, name  # unmangled: extern "C"
+
+
+def test_error_strings_are_the_reference_messages():
+    import myyuv_hip
+    assert myyuv_hip.strerror(2) == "Level of quality must be between 1 and 100"
+    assert myyuv_hip.strerror(3) == "Error. width % 8 must be 0"
+    assert myyuv_hip.strerror(4) == "Error. height % 8 must be 0"
+    assert myyuv_hip.strerror(6) == "DCTYUV load bad size"
+    assert myyuv_hip.strerror(7) == "DCTYUVPlane load bad size"
+    assert myyuv_hip.strerror(8) == "DCTYUVPlane load chunks_sizes_size bad size"
+    assert myyuv_hip.strerror(9) == "DCTYUVPlane load content_size bad size"
+    assert myyuv_hip.strerror(10) == "Huffman bad code"
+    assert myyuv_hip.strerror(11) == "Huffman unknown symbol"
+
+
+def test_payload_bound_covers_worst_case(oracle):
+    import myyuv_hip
+    for w, h in ((16, 16), (992, 736), (4032, 3008), (8192, 8192)):
+        assert myyuv_hip.payload_bound(w, h) >= oracle.lib().oracle_payload_bound(w, h)
+        assert myyuv_hip.payload_bound(w, h) % 4 == 0
+
+
+def test_no_cpu_fallback_without_gpu():
+    """On a machine without a GPU the product path fails loudly (no silent CPU
+    fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    import myyuv_hip
+    with pytest.raises(myyuv_hip.CodecError) as e:
+        myyuv_hip.Codec(0)
+    assert e.value.code == myyuv_hip.E_NO_DEVICE
+
+
+def test_host_library_and_cli_are_built():
+    for f in ("libmyyuv_hip.so", "libmyyuv_amd.so", "myyuv_cli"):
+        assert os.path.exists(os.path.join(PKG, f)), f
+    out = subprocess.run(["nm", "-DC", "--defined-only", os.path.join(PKG, "libmyyuv_amd.so")],
+                         capture_output=True, text=True, check=True).stdout
+    for sym in ("myyuvDCT::compress_DCT_planar", "myyuvDCT::decompress_DCT_planar",
+                "myyuv::YUV::compress_map", "myyuv::YUV::decompress_map", "myyuv::YUV::load",
+                "myyuv::YUV::dump"):
+        assert sym in out, sym

@@ -1,0 +1,99 @@
+"""myyuv_cli drop-in: same command line and output files as the reference CLI
+(myyuv_cli/main.cpp).  CPU tests cover the paths with no codec work (-info,
+argument errors) against the reference CLI built in oracle/_ref; GPU tests run
+compress / decompress and compare the files byte for byte."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, PKG, ROOT
+
+CLI = os.path.join(PKG, "myyuv_cli")
+REF_CLI = os.path.join(ROOT, "oracle", "_ref", "myyuv_cli_ref")
+SMALL = os.path.join(GOLDEN, "chef-with-trumpet.myyuv")
+C50 = os.path.join(GOLDEN, "chef-with-trumpet-DCT-50.myyuv")
+
+
+def run(exe, *args):
+    return subprocess.run([exe, *args], capture_output=True, text=True)
+
+
+def need_ref():
+    if not os.path.exists(REF_CLI):
+        pytest.skip("reference CLI not built (make -C oracle ref)")
+
+
+@pytest.mark.parametrize("path", [SMALL, C50])
+def test_info_matches_reference(path):
+    need_ref()
+    a, b = run(CLI, path, "-info"), run(REF_CLI, path, "-info")
+    assert a.returncode == b.returncode == 0
+    assert a.stdout == b.stdout
+
+
+def test_argument_errors_match_reference(tmp_path):
+    need_ref()
+    for args in ([SMALL, "-bogus"], [SMALL, "-compress"], [SMALL, "-compress", "DCT", "50"],
+                 [SMALL, "-decompress", "-o", str(tmp_path / "x")], [C50, "-decompress", "x"]):
+        a, b = run(CLI, *args), run(REF_CLI, *args)
+        assert a.returncode == b.returncode, args
+        assert a.stdout.splitlines()[0] == b.stdout.splitlines()[0], args
+
+
+def test_no_args_prints_usage():
+    r = run(CLI, SMALL)
+    assert r.returncode == 0 and "Usage" in r.stdout
+
+
+def test_unknown_magic_fails(tmp_path):
+    p = tmp_path / "junk.bin"
+    p.write_bytes(b"XXjunk")
+    r = run(CLI, str(p), "-info")
+    assert r.returncode != 0
+    assert "Unknown image format (magic)" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,gold", [(["50"], "chef-with-trumpet-DCT-50.myyuv"),
+                                    (["90", "90", "90"], "chef-with-trumpet-DCT-90.myyuv")])
+def test_cli_compress_matches_golden(tmp_path, q, gold):
+    out = tmp_path / "out.myyuv"
+    r = run(CLI, SMALL, "-compress", "DCT", *q, "-o", str(out))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("YUV DCT compression (") and r.stdout.rstrip().endswith("Success!")
+    assert out.read_bytes() == open(os.path.join(GOLDEN, gold), "rb").read()
+
+
+@pytest.mark.gpu
+def test_cli_decompress_matches_reference(tmp_path, oracle, golden):
+    out = tmp_path / "dec.myyuv"
+    r = run(CLI, C50, "-decompress", "-o", str(out))
+    assert r.returncode == 0, r.stderr
+    g = golden("chef-with-trumpet-DCT-50.myyuv")
+    exp = g.decompressed(oracle.decompress(g.data, g.width, g.height, tuple(g.params))).dumps()
+    assert out.read_bytes() == exp
+    if os.path.exists(REF_CLI):
+        ref_out = tmp_path / "ref.myyuv"
+        assert run(REF_CLI, C50, "-decompress", "-o", str(ref_out)).returncode == 0
+        assert out.read_bytes() == ref_out.read_bytes()
+
+
+@pytest.mark.gpu
+def test_cli_roundtrip_big(tmp_path):
+    big = os.path.join(GOLDEN, "chef-with-trumpet-big-DCT-50.myyuv")
+    dec, rec = tmp_path / "dec.myyuv", tmp_path / "rec.myyuv"
+    assert run(CLI, big, "-decompress", "-o", str(dec)).returncode == 0
+    assert run(CLI, str(dec), "-compress", "DCT", "50", "-o", str(rec)).returncode == 0
+    import hashlib
+    assert hashlib.sha256(dec.read_bytes()).hexdigest() == \
+        "5e7769191188285cc127c6b4da900b3420f064191f707383c82128c14e497e5c"
+    assert hashlib.sha256(rec.read_bytes()).hexdigest() == \
+        "18405d3e6f79a0054fbdb166ae76f58d8dbffc605263f4c3c0b65e51babefbf7"
+
+
+@pytest.mark.gpu
+def test_cli_bad_quality_fails_like_reference(tmp_path):
+    r = run(CLI, SMALL, "-compress", "DCT", "0", "-o", str(tmp_path / "x"))
+    assert r.returncode != 0
+    assert "Compression parameters for DCT must range between [1..100]" in r.stderr

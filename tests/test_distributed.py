@@ -1,0 +1,74 @@
+"""Multi-rank batch path on CPU (gloo): frames sharded round-robin, compressed
+per rank, streams gathered to rank 0 in frame order (yuv-manipulations-2_amd/
+batch.py).  The codec here is the CPU restatement; on the GPU box the same
+driver runs with the HIP codec over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def frame(f, w=64, h=48):
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    import synth
+    return synth.splitmix64_bytes(w * h * 3 // 2, seed=1000 + f).tobytes()
+
+
+def _worker(rank, world, port, n_frames, q, out):
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    import torch
+    import torch.distributed as dist
+    import batch
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def compress(f):
+            pay = O.compress(frame(f), 64, 48, q)
+            t = torch.frombuffer(bytearray(pay + bytes(16)), dtype=torch.uint8)  # padded slot
+            return t, torch.tensor([len(pay)], dtype=torch.int32)
+        got = batch.run_batch(dist, None, compress, n_frames, world, rank, torch.device("cpu"))
+        if rank == 0:
+            out.put([bytes(t.numpy()) for t in got])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_frames", [(2, 6), (2, 5), (3, 7)])
+def test_batch_gather_gloo(world, n_frames):
+    from oracle import oracle as O
+    q = (50, 60, 70)
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, q, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = out.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(got) == n_frames
+    for f in range(n_frames):
+        assert got[f] == O.compress(frame(f), 64, 48, q), f
+
+
+def test_shard_is_round_robin():
+    import batch
+    assert batch.shard(10, 4, 1) == [1, 5, 9]
+    assert sorted(sum((batch.shard(11, 3, r) for r in range(3)), [])) == list(range(11))

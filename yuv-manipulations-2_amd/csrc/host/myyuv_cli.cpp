@@ -1,0 +1,155 @@
+// myyuv_cli.cpp — drop-in for the reference CLI's YUV commands
+// (myyuv_cli/main.cpp:138-253) on the MI355X codec:
+//   myyuv_cli in.myyuv -info
+//   myyuv_cli in.myyuv -compress DCT q [q [q]] -o out.myyuv
+//   myyuv_cli in.myyuv -decompress -o out.myyuv
+// Same argument rules, quality fill (the last value repeats, main.cpp:64-75),
+// same integer-millisecond timing line and "Success!" (main.cpp:11-41, 241),
+// same failure mode (usage, then the exception propagates).  BMP input
+// (-to_yuv) is outside the DCT path and reported as unsupported.
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <iostream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "myyuv_yuv.hpp"
+
+namespace {
+
+float elapsed_ms(const std::function<void()>& f) {
+  const auto t0 = std::chrono::high_resolution_clock::now();
+  f();
+  const auto t1 = std::chrono::high_resolution_clock::now();
+  return (float)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count();
+}
+
+void usage() {
+  std::cout << "myyuv_cli (MI355X DCT codec): inspect and DCT-compress/decompress .myyuv images.\n"
+            << "Usage:\n"
+            << "  myyuv_cli IMAGE.myyuv -info\n"
+            << "  myyuv_cli IMAGE.myyuv -compress DCT Q [Q [Q]] -o OUT.myyuv   (Q in 1..100, per plane Y U V)\n"
+            << "  myyuv_cli IMAGE.myyuv -decompress -o OUT.myyuv\n"
+            << "\nYUV formats:\nIYUV\n\nCompression formats for YUV:\nDCT\n"
+            << "\nExample:\n  myyuv_cli image.myyuv -compress DCT 50 -o image-DCT-50.myyuv\n";
+}
+
+myyuv::YUV compress_dct(const myyuv::YUV& yuv, const std::vector<std::string>& params) {
+  if (params.size() > 3)
+    throw std::runtime_error("Error. Too many compression parameters. Can't be more than 3 parameters.");
+  if (params.empty()) throw std::runtime_error("Error. Too few compression parameters. Must be at least one.");
+  uint8_t q[3];
+  for (size_t i = 0; i < 3; i++) {
+    const int v = std::stoi(params[i < params.size() ? i : params.size() - 1]);
+    if (v < 1 || v > 100)
+      throw std::runtime_error("Error. Compression parameters for DCT must range between [1..100].");
+    q[i] = (uint8_t)v;
+  }
+  return yuv.compress(myyuv::YUV::Compressions::DCT, q, 3);
+}
+
+int run_yuv(const myyuv::YUV& yuv, size_t a, const std::vector<std::string>& args) {
+  const std::string& cmd = args[a];
+  if (cmd == "-info") {
+    const auto& h = yuv.header;
+    std::cout << "Type: " << h.type[0] << h.type[1] << '\n'
+              << "FourCC Format: 0x" << std::hex << h.fourcc_format << std::dec << '\n'
+              << "File size: " << (sizeof(h) + h.compression_params_size + h.data_size) << '\n'
+              << "Data size: " << h.data_size << '\n'
+              << "Compression: " << h.compression << '\n'
+              << "Compression params size: " << h.compression_params_size << '\n'
+              << "Width: " << h.width << '\n'
+              << "Height: " << h.height << '\n'
+              << "Valid: " << yuv.isValid() << '\n';
+    return 0;
+  }
+  if (cmd == "-compress") {
+    a++;
+    if (a >= args.size()) {
+      std::cout << "Invalid arguments. Specify compression algorithm, compression parameters and output.\n";
+      usage();
+      return 1;
+    }
+    const std::string algo = args[a++];
+    if (algo != "DCT") throw std::runtime_error("Compression not registered: " + algo);
+    std::vector<std::string> params;
+    while (a < args.size() && args[a] != "-o") params.push_back(args[a++]);
+    a++;
+    if (a >= args.size()) {
+      std::cout << "Invalid argument, last arguments must be `-o /path/to/new_image.myyuv`\n";
+      usage();
+      return 1;
+    }
+    std::string label = " ";
+    for (const auto& p : params) label += p + " ";
+    myyuv::YUV out;
+    const float ms = elapsed_ms([&] { out = compress_dct(yuv, params); });
+    std::cout << "YUV DCT compression (" << label << ") : " << ms << " ms\n";
+    out.dump(args[a]);
+    return 0;
+  }
+  if (cmd == "-decompress") {
+    if (!yuv.isCompressed()) {
+      std::cout << "Nothing to decompress, image is not compressed\n";
+      return 1;
+    }
+    a++;
+    if (args.size() != a + 2) {
+      std::cout << "Invalid arguments amount. " << (a + 2) << " is required\n";
+      usage();
+      return 1;
+    }
+    if (args[a] != "-o") {
+      std::cout << a << " argument must be `-o` instead of " << args[a] << '\n';
+      usage();
+      return 1;
+    }
+    myyuv::YUV out;
+    const float ms = elapsed_ms([&] { out = yuv.decompress(); });
+    std::cout << "YUV DCT decompression : " << ms << " ms\n";
+    out.dump(args[a + 1]);
+    return 0;
+  }
+  std::cout << "Invalid command " << cmd << '\n';
+  usage();
+  return 1;
+}
+
+int run(int argc, char* argv[]) {
+  if (argc <= 2) {
+    usage();
+    return 0;
+  }
+  const std::vector<std::string> args(argv, argv + argc);
+  const std::string& path = args[1];
+  char magic[2] = {0, 0};
+  {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("Error opening file to read " + path);
+    f.read(magic, 2);
+  }
+  int rc;
+  if (magic[0] == 'Y' && magic[1] == 'U') {
+    rc = run_yuv(myyuv::YUV(path), 2, args);
+  } else if (magic[0] == 'B' && magic[1] == 'M') {
+    throw std::runtime_error("BMP input is not handled by the MI355X build (DCT path only): " + path);
+  } else {
+    throw std::runtime_error("Unknown image format (magic) " + path);
+  }
+  if (rc == 0) std::cout << "Success!\n";
+  return rc;
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+  try {
+    return run(argc, argv);
+  } catch (...) {
+    usage();
+    throw;
+  }
+}
