@@ -9,7 +9,7 @@ compressed stream resident in HBM: compress_device -> decompress_device on one
 stream.  value = megapixels (luma W*H) of all ranks' steps / max-over-ranks
 wall time of the K timed steps.
 
-roofline: K1 fdct_quant_zz (the block-transform kernel of the north star),
+roofline: K1 fdct_quant (the block-transform kernel of the north star),
 algorithmic bytes = 3 B per sample (1 B u8 in + 2 B int16 out) x W*H*3/2
 samples per launch, divided by its average launch time from HIP events on the
 launch stream over the timed region.  `traffic` = FETCH_SIZE*2 + WRITE_SIZE
@@ -73,7 +73,7 @@ def load_traffic():
     try:
         with open(best) as f:
             d = json.load(f)
-        return d.get("fdct_quant_zz", {}).get("hbm_bytes_per_launch")
+        return d.get("fdct_quant", {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -208,7 +208,7 @@ def main():
     if rank == 0:
         ms_step = t / args.steps * 1e3
         value = world * args.steps * mp / t
-        k1_ms, k1_n = stats.get("fdct_quant_zz", (0.0, 0))
+        k1_ms, k1_n = stats.get("fdct_quant", (0.0, 0))
         roof = None
         if k1_n:
             avg_s = k1_ms / k1_n / 1e3
@@ -216,7 +216,7 @@ def main():
             achieved = alg / avg_s / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": load_traffic(), "kernel": "fdct_quant_zz",
+                    "traffic": load_traffic(), "kernel": "fdct_quant",
                     "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2)}
         for k, (kms, kn) in stats.items():
             if kn:

@@ -105,21 +105,27 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
 
 /* Per-kernel timing (HIP events around each launch, on the launch stream).
  * enable=1 starts recording; myyuv_hip_kernel_stats fills, per kernel id
- * (MYYUV_K_*), the summed milliseconds and launch count since enabling. */
-#define MYYUV_K_FDCT 0       /* K1 fdct_quant_zz */
-#define MYYUV_K_HUFF_ENC 1   /* K2 huff_encode */
-#define MYYUV_K_SCAN 2       /* scan of chunk sizes (both directions) */
+ * (MYYUV_K_*), the summed milliseconds and launch count since enabling.
+ * Times are kernel execution times (start/stop stamped from the dispatch
+ * packet, as rocprofv3's kernel trace). */
+#define MYYUV_K_FDCT 0       /* K1 fdct_quant */
+#define MYYUV_K_HUFF_ENC 1   /* K2 huff_encode (CAP=8 pass over every block) */
+#define MYYUV_K_SCAN 2       /* scan of chunk sizes, per-tile pass (both directions) */
 #define MYYUV_K_COMPACT 3    /* K4 compaction into the DCTYUV stream */
 #define MYYUV_K_PARSE 4      /* decode-side stream header parse */
 #define MYYUV_K_HUFF_DEC 5   /* K5 huff_decode */
 #define MYYUV_K_IDCT 6       /* K6 dequant_idct */
-#define MYYUV_K_COUNT 7
+#define MYYUV_K_HUFF_WIDE 7  /* K2 overflow pass (CAP=64, worklist) */
+#define MYYUV_K_SCAN_SUMS 8  /* scan of chunk sizes, tile-prefix pass */
+#define MYYUV_K_COUNT 9
 int myyuv_hip_profile(myyuv_hip_handle h, int enable);
 int myyuv_hip_kernel_stats(myyuv_hip_handle h, double ms[MYYUV_K_COUNT],
                            int64_t launches[MYYUV_K_COUNT]);
 
 /* Block-level entry points for known-answer tests (device round trip of one
- * batch of blocks).  coef is zig-zag ordered int16[64] per block. */
+ * batch of blocks).  coef is zig-zag ordered int16[64] per block; the encoder
+ * rejects (MYYUV_E_ARG) coefficients outside [-1024, 1023], the 11-bit range
+ * the chunk format carries and K1 produces (DCT.cpp:276). */
 int myyuv_gpu_fdct_blocks(myyuv_hip_handle h, const uint8_t* px, uint32_t nblocks,
                           const float qtable[64], int16_t* coef_zz);
 int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle h, const int16_t* coef_zz, uint32_t nblocks,

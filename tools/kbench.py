@@ -32,12 +32,16 @@ def main():
     d_pay = torch.empty(cap, dtype=torch.uint8, device=dev)
     d_size = torch.zeros(1, dtype=torch.int32, device=dev)
     codec.reserve(w, h)
+    rc = None
     for it in range(2):
         codec.profile(it == 1)
         for _ in range(steps if it else 3):
             codec.compress_device(d_in.data_ptr(), w, h, q, d_pay.data_ptr(), cap, d_size.data_ptr(), sp)
             codec.decompress_device(d_pay.data_ptr(), d_size.data_ptr(), cap, w, h, q, d_out.data_ptr(), sp)
-        rc, bad = codec.sync_status(sp)
+        try:
+            rc, bad = codec.sync_status(sp)
+        except Exception as e:  # ablation builds may produce invalid streams
+            rc = repr(e)
     stats = codec.kernel_stats()
     ok = bytes(d_out.cpu().numpy()) == expect
     print(f"{os.environ.get('MYYUV_HIP_LIB', 'default')}: rc={rc} roundtrip_equal={ok}")

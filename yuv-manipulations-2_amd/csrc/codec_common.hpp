@@ -46,14 +46,46 @@ struct FrameGeom {
   uint32_t bw[3];         // blocks per block-row
   uint32_t cum[4];        // cumulative block counts: plane p owns [cum[p], cum[p+1])
   uint32_t poff[3];       // byte offset of plane p in the IYUV frame
-  uint32_t gpr[3];        // transform groups (8 blocks of one block-row) per block-row
-  uint32_t gcum[4];       // cumulative transform groups
+  uint32_t wcum[4];       // transform workgroups (64 blocks of one plane) per plane, cumulative
+  uint64_t bmag[3];       // ceil(2^64 / bw[p]) (0 for bw = 1): block_row() divides by it
 };
 
-// Tables the kernels read per call (uploaded once per quality triple).
+// by = floor(local / bw) = high 64 bits of local * ceil(2^64 / bw): the
+// product overshoots local / bw by less than local / 2^64, below the 1 / bw
+// slack, so the floor is exact for every 32-bit local.
+__host__ __device__ __forceinline__ uint32_t block_row(const FrameGeom& G, int p, uint32_t local) {
+  const uint64_t m = G.bmag[p];
+  if (m == 0) return local;
+  const uint64_t lo = (uint64_t)local * (uint32_t)m;
+  const uint64_t hi = (uint64_t)local * (uint32_t)(m >> 32) + (lo >> 32);
+  return (uint32_t)(hi >> 32);
+}
+
+// Per-quality tables, passed to K1/K6 by value (kernel arguments).
 struct QTables {
   float q[3][64];     // natural order, DCT.cpp:286-290
-  float qzz[3][64];   // zig-zag order: qzz[p][z] = q[p][zigzag[z]]
+  float r[3][64];     // 1.0f / q, correctly rounded (K1's division-free fast path)
+  float near[3][4];   // K1 near-tie threshold of the lane owning rows 2j, 2j+1:
+                      // fma(max r over those rows, kNearScale, -0.25)
 };
+
+// 2 * Ymax * 2^-21 with Ymax = 1100 > the largest |Y| an 8x8 block of
+// x - 128 in [-128, 127] can produce (1024 at DC, < 850 elsewhere): K1's
+// near-tie window per unit of 1/Q (k_transform.hip).
+constexpr float kNearScale = 2.0f * 1100.0f * 0x1p-21f;
+
+// Coefficient layout shared by K1, K2, K5 and K6: per block 64 int16 in
+// NATURAL (row-major) order, word w = coefficients 2w, 2w+1; words grouped in
+// quads (16 B) and the quads of 64 consecutive blocks interleaved, so that
+//   quad c (words 4c..4c+3, i.e. row c/2's half) of block g is uint4 element
+//   ((g >> 6) * 8 + c) * 64 + (g & 63).
+// A lane-per-block wave reads one quad of 64 blocks as 1 KiB contiguous; K1/K6
+// (four lanes per block, two rows each) write/read 256 B runs.  The zig-zag
+// scan is a fixed permutation applied with static register indices where the
+// coefficients are consumed (K2) or produced (K5).
+constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
+__host__ __device__ __forceinline__ uint32_t coef_quad(uint32_t g, uint32_t c) {
+  return ((g >> 6) * 8u + c) * 64u + (g & 63u);
+}
 
 }  // namespace myyuv_gpu

@@ -17,8 +17,10 @@
 //      the bit-serial loop would stop at, including on malformed tables
 //      (uint8 arithmetic of `first` kept), and the bit budget checks give the
 //      same "bad code" / "unknown symbol" outcomes.
-// Output: 64 int16 per block in zig-zag order (decode order), zero-filled
-// after the last symbol, in the block-interleaved layout of K1/K6.
+// Output: 64 int16 per block, zero-filled after the last symbol, decoded in
+// zig-zag order into LDS and written out in natural order (the inverse scan
+// is a compile-time permutation of registers) in the quad layout of
+// codec_common.hpp that K6 reads.
 #include "codec_common.hpp"
 #include "k_stream.hpp"
 
@@ -28,6 +30,17 @@ namespace {
 
 constexpr int kStageWords = (kWave * kMaxChunk) / 4 + 4;
 constexpr int kOutStride = 65;  // words; conflict-free for both access directions
+
+// inverse zig-zag: c_izz[n] = position of natural index n in the scan
+struct IzzTable {
+  uint8_t v[64];
+  constexpr IzzTable() : v{} {
+    constexpr uint8_t zz[64] = MYYUV_ZIGZAG;
+    for (int z = 0; z < 64; z++) v[zz[z]] = (uint8_t)z;
+  }
+};
+constexpr IzzTable kIzz{};
+constexpr const uint8_t* c_izz = kIzz.v;
 
 __device__ __forceinline__ void record_error(unsigned long long* err, uint64_t key, int code) {
   atomicMin(err, (unsigned long long)((key << 8) | (uint64_t)code));
@@ -151,7 +164,7 @@ __global__ __launch_bounds__(64) void k_huff_decode(const uint8_t* __restrict__ 
                                                    const uint32_t* __restrict__ tile_pre,
                                                    FrameGeom G, uint32_t tiles_p0,
                                                    uint32_t tiles_p1,
-                                                   uint32_t* __restrict__ coefw,
+                                                   uint4* __restrict__ coef,
                                                    unsigned long long* __restrict__ err) {
   __shared__ uint32_t stage[kStageWords];
   __shared__ uint32_t symw[32 * kWave];
@@ -230,12 +243,23 @@ __global__ __launch_bounds__(64) void k_huff_decode(const uint8_t* __restrict__ 
   }
   __syncthreads();
 
-  // ---- write-out in the block-interleaved layout K6 reads: word w of block
-  // g at ((g>>6)*32 + w)*64 + (g&63) (256 contiguous bytes per store).
+  // ---- write-out: zig-zag words from LDS, natural words to the quad layout
+  // (Huffman.cpp:148-153 de-zig-zag; 1 KiB contiguous per quad store)
   if (live) {
-    uint32_t* dst = coefw + (size_t)(g >> 6) * 32 * 64 + (g & 63);
-#pragma unroll 8
-    for (int w = 0; w < 32; w++) dst[w * 64] = outw[w * kOutStride + lane];
+    uint32_t zw[32];
+#pragma unroll
+    for (int w = 0; w < 32; w++) zw[w] = outw[w * kOutStride + lane];
+    uint32_t nw[32];
+#pragma unroll
+    for (int m = 0; m < 32; m++) {
+      const int z0 = c_izz[2 * m], z1 = c_izz[2 * m + 1];
+      const uint32_t lo = (zw[z0 >> 1] >> (16 * (z0 & 1))) & 0xFFFFu;
+      const uint32_t hi = (zw[z1 >> 1] >> (16 * (z1 & 1))) & 0xFFFFu;
+      nw[m] = lo | (hi << 16);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; c++)
+      coef[coef_quad(g, c)] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
   }
 }
 

@@ -8,15 +8,17 @@
 // is LDS latency, hence a small per-lane LDS image (64 B for the CAP=8 pass:
 // 32 waves per CU) and no pointer chasing on the per-symbol path:
 //   1. distinct symbols of the message (zig-zag order, trailing zeros
-//      stripped; msz comes from K1) in first-occurrence order with counts,
+//      stripped) in first-occurrence order with counts,
 //      found through a small open-addressing table (slot ids) -> KC;
 //   2. replay of std::unordered_map's iteration order over KC, libstdc++
 //      binary-heap Huffman merges, code lengths, canonical order and codes;
 //   3. serialisation (header, 11-bit table groups, code bits) into the
 //      block's 160-B output slot.
-// Coefficients come in K1's block-interleaved layout: word w (zig-zag
-// coefficients 2w, 2w+1) of block g at ((g>>6)*32 + w)*64 + (g&63), so the
-// wave reads 256 contiguous bytes per symbol pair.
+// Coefficients come in K1's natural-order quad layout (codec_common.hpp): a
+// lane loads its block's 8 quads (the wave reads 1 KiB contiguous per quad)
+// into 32 registers; the zig-zag scan (Huffman.cpp:32-34, :176-182) is the
+// compile-time permutation behind CoefRegs::sym(), and the message length
+// (trailing zig-zag zeros stripped, Huffman.cpp:184-190) is found the same way.
 // CAP bounds the distinct symbols: the CAP=8 pass runs on every block and
 // appends the blocks with more to a worklist that the CAP=64 pass drains.
 //
@@ -268,35 +270,48 @@ struct BitWriter {
   }
 };
 
-// The lane's block's coefficient words (zig-zag coefficients 2w, 2w+1 in
-// word w), loaded once into registers: both symbol loops below are unrolled
-// so every access is a static register index.
-struct CoefReader {
-  const uint32_t* w;  // &coefw[((g>>6)*32 + 0)*64 + (g&63)], words kWave apart
-};
+// The lane's block's coefficients (natural order, word w = coefficients 2w,
+// 2w+1), loaded once into registers: every loop over positions below is
+// unrolled, so sym(i) — the i-th coefficient in zig-zag order — is a static
+// register index and half.
+constexpr uint8_t c_zz[64] = MYYUV_ZIGZAG;
+
 struct CoefRegs {
   uint32_t w[32];
-  __device__ __forceinline__ void load(const CoefReader& C, int wave_msz) {
+  __device__ __forceinline__ void load(const uint4* __restrict__ coef, uint32_t g) {
 #pragma unroll
-    for (int k = 0; k < 32; k++) w[k] = (2 * k < wave_msz) ? C.w[k * kWave] : 0u;
+    for (int c = 0; c < 8; c++) {
+      const uint4 v = coef[coef_quad(g, c)];
+      w[4 * c] = v.x;
+      w[4 * c + 1] = v.y;
+      w[4 * c + 2] = v.z;
+      w[4 * c + 3] = v.w;
+    }
   }
   __device__ __forceinline__ int sym(int i) const {
-    return (int)(int16_t)(w[i >> 1] >> (16 * (i & 1)));
+    const int n = c_zz[i];
+    return (int)(int16_t)(w[n >> 1] >> (16 * (n & 1)));
+  }
+  // 1 + zig-zag index of the last nonzero coefficient (0: all zero)
+  __device__ __forceinline__ int msz() const {
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      if (sym(i) != 0) m = i + 1;
+    return m;
   }
 };
 
 // The whole per-block program.  Returns false (and writes nothing) when the
 // block has more than CAP distinct symbols.
 template <int CAP>
-__device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefReader& C, int msz, int wave_msz,
+__device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefRegs& R, int msz, int wave_msz,
                              uint32_t* __restrict__ slot, uint8_t* __restrict__ size_out) {
 #ifdef MYYUV_STAMPS
   unsigned long long _tprev = 0;
 #endif
   STAMP(0);
   // ---------------- 1. distinct symbols in first-occurrence order ----------------
-  CoefRegs R;
-  R.load(C, wave_msz);
 #pragma unroll
   for (int w = 0; w < Layout<CAP>::kTWords; w++) I.wordAt(Layout<CAP>::kT + w) = 0u;
   int n = 0;
@@ -498,10 +513,9 @@ __device__ __forceinline__ int wave_max(int v) {
 
 // Fast pass over every block (CAP=8); blocks with more distinct symbols are
 // appended to `work` for k_huff_encode_wide.
-//   coefw: block-interleaved coefficient words (see top); msz: [n] u8;
+//   coef: natural-order quads (codec_common.hpp);
 //   slots: [ceil(n/64)][40][64] u32; sizes: [n] u8.
-__global__ __launch_bounds__(64) void k_huff_encode(const uint32_t* __restrict__ coefw,
-                                                   const uint8_t* __restrict__ mszs,
+__global__ __launch_bounds__(64) void k_huff_encode(const uint4* __restrict__ coef,
                                                    uint32_t nblocks,
                                                    uint32_t* __restrict__ slots,
                                                    uint8_t* __restrict__ sizes,
@@ -512,13 +526,14 @@ __global__ __launch_bounds__(64) void k_huff_encode(const uint32_t* __restrict__
   const int lane = threadIdx.x;
   const uint32_t g = blockIdx.x * kWave + lane;
   const bool live = g < nblocks;
-  const int msz = live ? mszs[g] : 0;
+  CoefRegs R;
+  R.load(coef, g);  // the buffer spans whole waves: dead lanes read padding
+  const int msz = live ? R.msz() : 0;
   const int wmsz = wave_max(msz);
   const Img<CAP> I{lds, lane};
-  const CoefReader C{coefw + (size_t)blockIdx.x * 32 * kWave + lane};
   bool ok = true;
   if (live)
-    ok = encode_block<CAP>(I, C, msz, max(wmsz, 1),
+    ok = encode_block<CAP>(I, R, msz, max(wmsz, 1),
                            slots + (size_t)blockIdx.x * (kSlotWords * kWave) + lane, sizes + g);
   const uint64_t ovf = __ballot(live && !ok);
   if (ovf) {
@@ -531,8 +546,7 @@ __global__ __launch_bounds__(64) void k_huff_encode(const uint32_t* __restrict__
 
 // Overflow pass (CAP=64): the blocks listed in `work` (count in *work_count),
 // 64 per workgroup; the grid is sized for the worst case, idle groups exit.
-__global__ __launch_bounds__(64) void k_huff_encode_wide(const uint32_t* __restrict__ coefw,
-                                                        const uint8_t* __restrict__ mszs,
+__global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict__ coef,
                                                         uint32_t* __restrict__ slots,
                                                         uint8_t* __restrict__ sizes,
                                                         const uint32_t* __restrict__ work,
@@ -544,12 +558,13 @@ __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint32_t* __restr
   if (blockIdx.x * kWave >= cnt) return;
   const bool live = i < cnt;
   const uint32_t g = live ? work[i] : 0;
-  const int msz = live ? mszs[g] : 0;
+  CoefRegs R;
+  R.load(coef, g);
+  const int msz = live ? R.msz() : 0;
   const int wmsz = wave_max(msz);
   if (!live) return;
   const Img<CAP> I{lds, (int)threadIdx.x};
-  const CoefReader C{coefw + (size_t)(g >> 6) * 32 * kWave + (g & 63)};
-  encode_block<CAP>(I, C, msz, max(wmsz, 1),
+  encode_block<CAP>(I, R, msz, max(wmsz, 1),
                     slots + (size_t)(g >> 6) * (kSlotWords * kWave) + (g & 63), sizes + g);
 }
 

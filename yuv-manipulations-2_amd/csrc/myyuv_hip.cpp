@@ -2,10 +2,11 @@
 //
 // Host side of the gfx950 codec: frame geometry, quantisation tables, the
 // per-context workspace, and the launch sequences
-//   compress:   K1 fdct_quant_zz -> K2 huff_encode -> scan -> K4 compact
+//   compress:   K1 fdct_quant -> K2 huff_encode -> scan -> K4 compact
 //   decompress: parse -> scan -> K5 huff_decode -> K6 dequant_idct
 // Every launch goes to one stream; nothing synchronises inside the
 // device-resident entry points, so frames pipeline back to back.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,11 +21,11 @@
 #include "myyuv_hip.h"
 
 namespace myyuv_gpu {
-__global__ void k_fdct_quant_zz(const uint8_t*, FrameGeom, const QTables*, uint32_t*, uint8_t*);
-__global__ void k_dequant_idct(const uint32_t*, FrameGeom, const QTables*, uint8_t*);
-__global__ void k_huff_encode(const uint32_t*, const uint8_t*, uint32_t, uint32_t*, uint8_t*,
+__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*);
+__global__ void k_dequant_idct(const uint4*, FrameGeom, const QTables*, uint8_t*);
+__global__ void k_huff_encode(const uint4*, uint32_t, uint32_t*, uint8_t*,
                               uint32_t*, uint32_t*);
-__global__ void k_huff_encode_wide(const uint32_t*, const uint8_t*, uint32_t*, uint8_t*,
+__global__ void k_huff_encode_wide(const uint4*, uint32_t*, uint8_t*,
                                    const uint32_t*, const uint32_t*);
 __global__ void k_scan_tiles(const uint8_t*, ScanSrc, const StreamDesc*, uint32_t*, uint32_t*);
 __global__ void k_scan_sums(uint32_t*, uint32_t, const StreamDesc*);
@@ -35,8 +36,7 @@ __global__ void k_parse(const uint8_t*, const uint32_t*, uint32_t, FrameGeom, St
                         unsigned long long*);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
-                              uint32_t*, unsigned long long*);
-extern __constant__ uint8_t c_izigzag[64];
+                              uint4*, unsigned long long*);
 #ifdef MYYUV_STAMPS
 extern __device__ unsigned long long g_k2_stamps[8];
 #endif
@@ -54,7 +54,6 @@ constexpr float kChromaQ[64] = {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 
                                 24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
                                 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
                                 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
-constexpr uint8_t kZigzag[64] = MYYUV_ZIGZAG;
 
 // DCT.cpp:286-290: Q = clamp(roundf(base * mul), 1, 255), mul in float.
 void make_qtable(int q, bool chroma, float out[64]) {
@@ -62,6 +61,18 @@ void make_qtable(int q, bool chroma, float out[64]) {
   const float fq = (float)q;
   const float mul = (fq >= 50.5f) ? (100.0f - fq) / 50.0f : 50.0f / fq;
   for (int i = 0; i < 64; i++) out[i] = std::min(std::max(std::roundf(base[i] * mul), 1.0f), 255.0f);
+}
+
+// Reciprocals and K1's per-lane near-tie thresholds from the Q tables.
+void finish_qtables(QTables& t, int planes) {
+  for (int p = 0; p < planes; p++) {
+    for (int n = 0; n < 64; n++) t.r[p][n] = 1.0f / t.q[p][n];
+    for (int j = 0; j < 4; j++) {
+      float rmax = 0.0f;
+      for (int n = 16 * j; n < 16 * j + 16; n++) rmax = std::max(rmax, t.r[p][n]);
+      t.near[p][j] = std::fma(rmax, kNearScale, -0.25f);
+    }
+  }
 }
 
 struct DevBuf {
@@ -87,7 +98,12 @@ struct DevBuf {
   }
 };
 
+constexpr uint8_t kZigzag[64] = MYYUV_ZIGZAG;
+
 uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// ceil(2^64 / bw) for FrameGeom::bmag; 0 marks bw = 1 (block_row returns local).
+uint64_t block_magic(uint32_t bw) { return bw > 1 ? ~0ull / bw + 1 : 0; }
 
 // Dimension checks in the reference's order: per plane, width then height
 // (applyDCTPlane / restoreDCTPlane, DCT.cpp:280-285, :338-343).
@@ -101,14 +117,13 @@ int make_geom(uint32_t w, uint32_t h, FrameGeom& G) {
   }
   std::memset(&G, 0, sizeof(G));
   G.cum[0] = 0;
-  G.gcum[0] = 0;
   for (int p = 0; p < 3; p++) {
     G.pw[p] = pw[p];
     G.ph[p] = ph[p];
     G.bw[p] = pw[p] / 8;
     G.cum[p + 1] = G.cum[p] + G.bw[p] * (ph[p] / 8);
-    G.gpr[p] = ceil_div(G.bw[p], 8);
-    G.gcum[p + 1] = G.gcum[p] + G.gpr[p] * (ph[p] / 8);
+    G.bmag[p] = block_magic(G.bw[p]);
+    G.wcum[p + 1] = G.wcum[p] + ceil_div(G.cum[p + 1] - G.cum[p], kWave);
   }
   G.poff[0] = 0;
   G.poff[1] = w * h;
@@ -121,7 +136,11 @@ int make_geom(uint32_t w, uint32_t h, FrameGeom& G) {
 struct myyuv_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf frame, coef, msz, slots, sizes, loff, tiles, payload, qt, err, psize, desc, work;
+  DevBuf frame, coef, slots, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
+  // quantisation tables of the last quality triple (host copy; qtd on the
+  // device, rewritten in stream order when the triple changes)
+  QTables qt;
+  hipStream_t qt_stream = nullptr;
   uint8_t q_cached[3] = {0, 0, 0};
   bool q_valid = false;
   // profiling
@@ -158,24 +177,24 @@ hipEvent_t take_event(myyuv_hip_ctx* c) {
   return e;
 }
 
-// Runs `launch` on `s`, bracketed by events when profiling.
-template <class F>
-int timed(myyuv_hip_ctx* c, int kid, hipStream_t s, F&& launch) {
+// Launches kernel `k` on `s`.  When profiling, the start/stop events are the
+// ones hipExtLaunchKernel stamps from the kernel's own dispatch packet: the
+// kernel's execution time (what rocprofv3's kernel trace reports), without
+// the few microseconds of queue latency a hipEventRecord bracket adds.
+template <class... KArgs, class... Args>
+int launch(myyuv_hip_ctx* c, int kid, void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t s,
+           Args... args) {
   hipEvent_t a = nullptr, b = nullptr;
   if (c->prof) {
     a = take_event(c);
     b = take_event(c);
-    (void)hipEventRecord(a, s);
   }
-  launch();
+  hipExtLaunchKernelGGL(k, grid, block, 0, s, a, b, 0, static_cast<KArgs>(args)...);
   if (hipPeekAtLastError() != hipSuccess) {
     (void)hipGetLastError();
     return MYYUV_E_HIP;
   }
-  if (c->prof) {
-    (void)hipEventRecord(b, s);
-    c->pending.push_back({kid, {a, b}});
-  }
+  if (c->prof) c->pending.push_back({kid, {a, b}});
   return 0;
 }
 
@@ -193,20 +212,22 @@ void drain_profile(myyuv_hip_ctx* c) {
   c->pending.clear();
 }
 
-int upload_qtables(myyuv_hip_ctx* c, const uint8_t q[3], hipStream_t s) {
+int set_qtables(myyuv_hip_ctx* c, const uint8_t q[3], hipStream_t s) {
   for (int p = 0; p < 3; p++)
     if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
-  if (c->q_valid && std::memcmp(c->q_cached, q, 3) == 0) return 0;
-  QTables t;
+  if (c->q_valid && std::memcmp(c->q_cached, q, 3) == 0 && c->qt_stream == s) return 0;
   for (int p = 0; p < 3; p++) {
-    make_qtable(q[p], p != 0, t.q[p]);
-    for (int z = 0; z < 64; z++) t.qzz[p][z] = t.q[p][kZigzag[z]];
+    make_qtable(q[p], p != 0, c->qt.q[p]);
   }
-  if (c->qt.grow(sizeof(QTables))) return MYYUV_E_HIP;
-  // the table buffer may still be read by queued kernels: order the update
-  // on the stream and wait for it (a quality change is rare).
-  if (hipStreamSynchronize(s) != hipSuccess) return MYYUV_E_HIP;
-  if (hipMemcpy(c->qt.p, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess) return MYYUV_E_HIP;
+  finish_qtables(c->qt, 3);
+  if (c->qtd.grow(sizeof(QTables))) return MYYUV_E_HIP;
+  // kernels queued on another stream may still read the old tables
+  if (c->qt_stream && c->qt_stream != s && hipStreamSynchronize(c->qt_stream) != hipSuccess)
+    return MYYUV_E_HIP;
+  // pageable source: the copy is staged before the call returns
+  if (hipMemcpyAsync(c->qtd.p, &c->qt, sizeof(QTables), hipMemcpyHostToDevice, s) != hipSuccess)
+    return MYYUV_E_HIP;
+  c->qt_stream = s;
   std::memcpy(c->q_cached, q, 3);
   c->q_valid = true;
   return 0;
@@ -217,8 +238,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   const uint32_t nwaves = ceil_div(nblk, kWave);
   const uint32_t ntiles = ceil_div(nblk, kScanTile);
   int e = 0;
-  e |= c->coef.grow((size_t)nwaves * 32 * kWave * 4);  // block-interleaved words
-  e |= c->msz.grow((size_t)nwaves * kWave);
+  e |= c->coef.grow((size_t)nwaves * kCoefQuadsPerWave * 16);  // natural-order quads
   e |= c->slots.grow((size_t)nwaves * kSlotWords * kWave * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
   e |= c->loff.grow((size_t)nblk * 4);
@@ -236,48 +256,39 @@ int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, hipStream_t s) {
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
   if (hipMemsetAsync(count, 0, 4, s) != hipSuccess) return MYYUV_E_HIP;
-  return timed(c, MYYUV_K_HUFF_ENC, s, [&] {
-    hipLaunchKernelGGL(k_huff_encode, dim3(ceil_div(nblk, kWave)), dim3(kWave), 0, s,
-                       c->coef.as<const uint32_t>(), c->msz.as<const uint8_t>(), nblk,
-                       c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(), list, count);
-    hipLaunchKernelGGL(k_huff_encode_wide, dim3(ceil_div(nblk, kWave)), dim3(kWave), 0, s,
-                       c->coef.as<const uint32_t>(), c->msz.as<const uint8_t>(),
-                       c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(), (const uint32_t*)list,
-                       (const uint32_t*)count);
-  });
+  int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(ceil_div(nblk, kWave)), dim3(kWave), s,
+                 c->coef.as<const uint4>(), nblk, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
+                 list, count);
+  e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(ceil_div(nblk, kWave)), dim3(kWave), s,
+              c->coef.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
+              (const uint32_t*)list, (const uint32_t*)count);
+  return e;
 }
 
 int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void* d_out,
                     uint32_t cap, uint32_t* d_size, hipStream_t s) {
   const uint32_t nblk = G.cum[3];
   const uint32_t ntiles = ceil_div(nblk, kScanTile);
-  const QTables* qt = c->qt.as<QTables>();
+  const QTables* qt = c->qtd.as<const QTables>();
   unsigned long long* err = c->err.as<unsigned long long>();
   int e = 0;
-  e |= timed(c, MYYUV_K_FDCT, s, [&] {
-    hipLaunchKernelGGL(k_fdct_quant_zz, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
-                       static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint32_t>(),
-                       c->msz.as<uint8_t>());
-  });
+  e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, dim3(G.wcum[3]), dim3(256), s,
+              static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>());
   e |= launch_huff_encode(c, nblk, s);
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
   for (int p = 0; p < 3; p++) S.pos[p] = G.cum[p];
-  e |= timed(c, MYYUV_K_SCAN, s, [&] {
-    hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(256), 0, s, c->sizes.as<const uint8_t>(),
-                       S, (const StreamDesc*)nullptr, c->loff.as<uint32_t>(),
-                       c->tiles.as<uint32_t>());
-    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, c->tiles.as<uint32_t>(), ntiles,
-                       (const StreamDesc*)nullptr);
-  });
+  e |= launch(c, MYYUV_K_SCAN, k_scan_tiles, dim3(ntiles), dim3(256), s,
+              c->sizes.as<const uint8_t>(), S, (const StreamDesc*)nullptr, c->loff.as<uint32_t>(),
+              c->tiles.as<uint32_t>());
+  e |= launch(c, MYYUV_K_SCAN_SUMS, k_scan_sums, dim3(1), dim3(256), s, c->tiles.as<uint32_t>(),
+              ntiles, (const StreamDesc*)nullptr);
   const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], 256), t1 = ceil_div(G.cum[2] - G.cum[1], 256),
                  t2 = ceil_div(G.cum[3] - G.cum[2], 256);
-  e |= timed(c, MYYUV_K_COMPACT, s, [&] {
-    hipLaunchKernelGGL(k_compact, dim3(t0 + t1 + t2), dim3(256), 0, s,
-                       c->slots.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
-                       c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
-                       static_cast<uint8_t*>(d_out), cap, d_size, err);
-  });
+  e |= launch(c, MYYUV_K_COMPACT, k_compact, dim3(t0 + t1 + t2), dim3(256), s,
+              c->slots.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
+              c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
+              static_cast<uint8_t*>(d_out), cap, d_size, err);
   return e ? MYYUV_E_HIP : 0;
 }
 
@@ -285,35 +296,27 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
                       const uint32_t* d_size, uint32_t cap, void* d_out, hipStream_t s) {
   const uint32_t nblk = G.cum[3];
   const uint32_t ntiles = ceil_div(nblk, kScanTile);
-  const QTables* qt = c->qt.as<QTables>();
+  const QTables* qt = c->qtd.as<const QTables>();
   unsigned long long* err = c->err.as<unsigned long long>();
   StreamDesc* desc = c->desc.as<StreamDesc>();
   const uint8_t* in = static_cast<const uint8_t*>(d_in);
   int e = 0;
-  e |= timed(c, MYYUV_K_PARSE, s, [&] {
-    hipLaunchKernelGGL(k_parse, dim3(1), dim3(64), 0, s, in, d_size, cap, G, desc, err);
-  });
+  e |= launch(c, MYYUV_K_PARSE, k_parse, dim3(1), dim3(64), s, in, d_size, cap, G, desc, err);
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
   for (int p = 0; p < 3; p++) S.pos[p] = 0;
-  e |= timed(c, MYYUV_K_SCAN, s, [&] {
-    hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(256), 0, s, in, S,
-                       (const StreamDesc*)desc, c->loff.as<uint32_t>(), c->tiles.as<uint32_t>());
-    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, c->tiles.as<uint32_t>(), ntiles,
-                       (const StreamDesc*)desc);
-  });
+  e |= launch(c, MYYUV_K_SCAN, k_scan_tiles, dim3(ntiles), dim3(256), s, in, S,
+              (const StreamDesc*)desc, c->loff.as<uint32_t>(), c->tiles.as<uint32_t>());
+  e |= launch(c, MYYUV_K_SCAN_SUMS, k_scan_sums, dim3(1), dim3(256), s, c->tiles.as<uint32_t>(),
+              ntiles, (const StreamDesc*)desc);
   const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], kWave),
                  t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
-  e |= timed(c, MYYUV_K_HUFF_DEC, s, [&] {
-    hipLaunchKernelGGL(k_huff_decode, dim3(t0 + t1 + t2), dim3(kWave), 0, s, in, d_size, cap,
-                       (const StreamDesc*)desc, c->loff.as<const uint32_t>(),
-                       c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<uint32_t>(), err);
-  });
-  e |= timed(c, MYYUV_K_IDCT, s, [&] {
-    hipLaunchKernelGGL(k_dequant_idct, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
-                       c->coef.as<const uint32_t>(), G, qt, static_cast<uint8_t*>(d_out));
-  });
+  e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2), dim3(kWave), s, in, d_size,
+              cap, (const StreamDesc*)desc, c->loff.as<const uint32_t>(),
+              c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<uint4>(), err);
+  e |= launch(c, MYYUV_K_IDCT, k_dequant_idct, dim3(G.wcum[3]), dim3(256), s,
+              c->coef.as<const uint4>(), G, qt, static_cast<uint8_t*>(d_out));
   return e ? MYYUV_E_HIP : 0;
 }
 
@@ -408,10 +411,7 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
     delete c;
     return MYYUV_E_HIP;
   }
-  uint8_t izz[64];
-  for (int z = 0; z < 64; z++) izz[kZigzag[z]] = (uint8_t)z;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(c_izigzag), izz, 64) != hipSuccess ||
-      c->err.grow(8) || c->psize.grow(4) || c->desc.grow(sizeof(StreamDesc)) ||
+  if (c->err.grow(8) || c->psize.grow(4) || c->desc.grow(sizeof(StreamDesc)) ||
       hipMemset(c->err.p, 0xFF, 8) != hipSuccess) {
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -427,8 +427,8 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   (void)hipStreamSynchronize(c->stream);
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
-  DevBuf* bufs[] = {&c->frame, &c->coef, &c->msz,    &c->slots, &c->sizes, &c->loff, &c->tiles,
-                    &c->payload, &c->qt,  &c->err,   &c->psize, &c->desc, &c->work};
+  DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff, &c->tiles,
+                    &c->payload, &c->err, &c->qtd,   &c->psize, &c->desc, &c->work};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -457,7 +457,7 @@ int myyuv_gpu_dct_compress_device(myyuv_hip_handle c, const void* d_in, uint32_t
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-  if ((e = reserve(c, G)) || (e = upload_qtables(c, q, s))) return e;
+  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
   return launch_compress(c, G, d_in, d_out, cap, d_size, s);
 }
 
@@ -474,7 +474,7 @@ int myyuv_gpu_dct_decompress_device(myyuv_hip_handle c, const void* d_in, const 
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-  if ((e = reserve(c, G)) || (e = upload_qtables(c, q, s))) return e;
+  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
   return launch_decompress(c, G, d_in, d_size, cap, d_out, s);
 }
 
@@ -503,7 +503,7 @@ int myyuv_gpu_dct_compress(myyuv_hip_handle c, const uint8_t* iyuv, uint32_t w, 
   hipStream_t s = c->stream;
   const size_t fbytes = (size_t)w * h * 3 / 2;
   const uint32_t bound = myyuv_dct_payload_bound(w, h);
-  if ((e = reserve(c, G)) || (e = upload_qtables(c, q, s))) return e;
+  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
   if (c->frame.grow(fbytes) || c->payload.grow(bound)) return MYYUV_E_HIP;
   if (reset_err(c, s)) return MYYUV_E_HIP;
   if (hipMemcpyAsync(c->frame.p, iyuv, fbytes, hipMemcpyHostToDevice, s) != hipSuccess)
@@ -547,7 +547,7 @@ int myyuv_gpu_dct_decompress(myyuv_hip_handle c, const uint8_t* payload, uint32_
   hipStream_t s = c->stream;
   const uint32_t cap = (size + 3) & ~3u;
   const size_t fbytes = (size_t)w * h * 3 / 2;
-  if ((e = reserve(c, G)) || (e = upload_qtables(c, q, s))) return e;
+  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
   if (c->frame.grow(fbytes) || c->payload.grow(cap)) return MYYUV_E_HIP;
   if (reset_err(c, s)) return MYYUV_E_HIP;
   if (hipMemsetAsync(static_cast<uint8_t*>(c->payload.p) + (cap - 4), 0, 4, s) != hipSuccess ||
@@ -622,38 +622,44 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
   G.pw[0] = 8;
   G.ph[0] = 8 * nblocks;
   G.bw[0] = 1;
+  G.bmag[0] = block_magic(1);
   G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
-  G.gpr[0] = 1;
-  G.gcum[1] = G.gcum[2] = G.gcum[3] = nblocks;
+  G.wcum[1] = G.wcum[2] = G.wcum[3] = ceil_div(nblocks, kWave);
   QTables t;
   std::memset(&t, 0, sizeof(t));
   std::memcpy(t.q[0], qtable, 256);
-  if (reserve(c, G) || c->frame.grow((size_t)nblocks * 64) || c->qt.grow(sizeof(QTables)))
+  finish_qtables(t, 1);
+  if (reserve(c, G) || c->frame.grow((size_t)nblocks * 64) || c->qtd.grow(sizeof(QTables)))
     return MYYUV_E_HIP;
   c->q_valid = false;
   if (hipStreamSynchronize(s) != hipSuccess ||
-      hipMemcpy(c->qt.p, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->qtd.p, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->frame.p, px, (size_t)nblocks * 64, hipMemcpyHostToDevice) != hipSuccess)
     return MYYUV_E_HIP;
-  hipLaunchKernelGGL(k_fdct_quant_zz, dim3(ceil_div(G.gcum[3], 4)), dim3(256), 0, s,
-                     c->frame.as<const uint8_t>(), G, c->qt.as<const QTables>(),
-                     c->coef.as<uint32_t>(), c->msz.as<uint8_t>());
-  std::vector<uint32_t> words((size_t)ceil_div(nblocks, kWave) * 32 * kWave);
+  hipLaunchKernelGGL(k_fdct_quant, dim3(G.wcum[3]), dim3(256), 0, s,
+                     c->frame.as<const uint8_t>(), G, c->qtd.as<const QTables>(), c->coef.as<uint4>());
+  std::vector<uint32_t> words((size_t)ceil_div(nblocks, kWave) * kCoefQuadsPerWave * 4);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(words.data(), c->coef.p, words.size() * 4, hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return MYYUV_E_HIP;
-  for (uint32_t g = 0; g < nblocks; g++)
-    for (int w = 0; w < 32; w++)
-      std::memcpy(coef_zz + (size_t)g * 64 + 2 * w,
-                  &words[((size_t)(g >> 6) * 32 + w) * kWave + (g & 63)], 4);
+  for (uint32_t g = 0; g < nblocks; g++) {
+    int16_t nat[64];
+    for (uint32_t c4 = 0; c4 < 8; c4++)
+      std::memcpy(nat + 8 * c4, &words[(size_t)coef_quad(g, c4) * 4], 16);
+    for (int z = 0; z < 64; z++) coef_zz[(size_t)g * 64 + z] = nat[kZigzag[z]];
+  }
   return 0;
 }
 
 int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uint32_t nblocks,
                                  uint8_t* chunks160, uint8_t* sizes) {
   if (!c || !coef_zz || !chunks160 || !sizes || nblocks == 0) return MYYUV_E_ARG;
+  // the chunk format carries 11-bit symbols (pack11bit, Huffman.cpp:36-52);
+  // K1 never produces others (DCT.cpp:276 asserts the range)
+  for (size_t i = 0; i < (size_t)nblocks * 64; i++)
+    if (coef_zz[i] < -1024 || coef_zz[i] > 1023) return MYYUV_E_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
@@ -662,20 +668,15 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
   if (reserve(c, G)) return MYYUV_E_HIP;
   const uint32_t nwaves = ceil_div(nblocks, kWave);
-  // host-side relayout into K1's output format: block-interleaved words + msz
-  std::vector<uint32_t> words((size_t)nwaves * 32 * kWave, 0u);
-  std::vector<uint8_t> msz((size_t)nwaves * kWave, 0);
+  // host-side relayout into K1's output format: natural-order quads
+  std::vector<uint32_t> words((size_t)nwaves * kCoefQuadsPerWave * 4, 0u);
   for (uint32_t g = 0; g < nblocks; g++) {
-    const int16_t* src = coef_zz + (size_t)g * 64;
-    int last = -1;
-    for (int i = 0; i < 64; i++)
-      if (src[i] != 0) last = i;
-    msz[g] = (uint8_t)(last + 1);
-    for (int w = 0; w < 32; w++)
-      std::memcpy(&words[((size_t)(g >> 6) * 32 + w) * kWave + (g & 63)], src + 2 * w, 4);
+    int16_t nat[64];
+    for (int z = 0; z < 64; z++) nat[kZigzag[z]] = coef_zz[(size_t)g * 64 + z];
+    for (uint32_t c4 = 0; c4 < 8; c4++)
+      std::memcpy(&words[(size_t)coef_quad(g, c4) * 4], nat + 8 * c4, 16);
   }
-  if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->msz.p, msz.data(), msz.size(), hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return MYYUV_E_HIP;
   if (launch_huff_encode(c, nblocks, s)) return MYYUV_E_HIP;
   std::vector<uint32_t> slots((size_t)nwaves * kSlotWords * kWave);

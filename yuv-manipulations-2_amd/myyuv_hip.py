@@ -18,9 +18,10 @@ E_ARG, E_QUALITY, E_WIDTH, E_HEIGHT, E_CAPACITY = 1, 2, 3, 4, 5
 E_DCTYUV_SIZE, E_PLANE_SIZE, E_PLANE_NBLK, E_PLANE_CONTENT = 6, 7, 8, 9
 E_BAD_CODE, E_UNKNOWN_SYMBOL, E_BAD_CHUNK, E_HIP, E_NO_DEVICE = 10, 11, 12, 13, 14
 
-KERNELS = ["fdct_quant_zz", "huff_encode", "scan", "compact", "parse", "huff_decode",
-           "dequant_idct"]
-K_FDCT, K_HUFF_ENC, K_SCAN, K_COMPACT, K_PARSE, K_HUFF_DEC, K_IDCT = range(7)
+KERNELS = ["fdct_quant", "huff_encode", "scan_tiles", "compact", "parse", "huff_decode",
+           "dequant_idct", "huff_encode_wide", "scan_sums"]
+(K_FDCT, K_HUFF_ENC, K_SCAN, K_COMPACT, K_PARSE, K_HUFF_DEC, K_IDCT, K_HUFF_WIDE,
+ K_SCAN_SUMS) = range(9)
 
 # the exported symbols include/myyuv_hip.h declares (checked by the CPU tests)
 EXPORTS = [
@@ -188,12 +189,12 @@ class Codec:
             raise CodecError(rc)
 
     def kernel_stats(self):
-        ms = (ctypes.c_double * 7)()
-        n = (ctypes.c_int64 * 7)()
+        ms = (ctypes.c_double * len(KERNELS))()
+        n = (ctypes.c_int64 * len(KERNELS))()
         rc = load().myyuv_hip_kernel_stats(self._h, ms, n)
         if rc:
             raise CodecError(rc)
-        return {KERNELS[i]: (ms[i], n[i]) for i in range(7)}
+        return {KERNELS[i]: (ms[i], n[i]) for i in range(len(KERNELS))}
 
     # -- block-level known-answer entry points --
     def fdct_blocks(self, px, qtable):
