@@ -1,34 +1,55 @@
-"""Diagnostic: K2 per-stage wave cycles (stamp build) on the bench frame."""
-import ctypes, os, sys
+"""Diagnostic: K2 per-stage cycles (stamp build, `make -C yuv-manipulations-2_amd stamps`)
+on the bench frame: fast pass summed per wave, wide pass mean and max per wave."""
+import ctypes
+import os
+import sys
+
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [R, os.path.join(R, 'yuv-manipulations-2_amd')]
 os.environ.setdefault('MYYUV_HIP_LIB', os.path.join(R, 'yuv-manipulations-2_amd/build/stamps/libmyyuv_hip.so'))
-import torch, myyuv_hip, myyuv_file, synth
+import torch  # noqa: E402
+import myyuv_file  # noqa: E402
+import myyuv_hip  # noqa: E402
+import synth  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
 c = myyuv_hip.Codec(0)
 L = myyuv_hip.load()
-names = ['', 'stage1', 'sync', 'map', 'heap+len', 'sort', 'emit']
-def run(raw, w, h, q, label):
+names = ['', 'symbols', 'map', 'heap+len', 'sort', 'emit']
+
+
+def run(raw, w, h, q, label, iters=10):
     d_in = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
     cap = myyuv_hip.payload_bound(w, h)
-    d_pay = torch.empty(cap, dtype=torch.uint8, device='cuda'); d_size = torch.zeros(1, dtype=torch.int32, device='cuda')
+    d_pay = torch.empty(cap, dtype=torch.uint8, device='cuda')
+    d_size = torch.zeros(1, dtype=torch.int32, device='cuda')
     sp = torch.cuda.current_stream().cuda_stream
-    for i in range(3):
-        c.compress_device(d_in.data_ptr(), w, h, (q,q,q), d_pay.data_ptr(), cap, d_size.data_ptr(), sp)
+    for _ in range(3):
+        c.compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay.data_ptr(), cap, d_size.data_ptr(), sp)
     c.sync_status(sp)
-    st = (ctypes.c_ulonglong * 8)()
+    st = (ctypes.c_ulonglong * 24)()
     L.myyuv_debug_k2_stamps(st)
     c.profile(True)
-    for i in range(10):
-        c.compress_device(d_in.data_ptr(), w, h, (q,q,q), d_pay.data_ptr(), cap, d_size.data_ptr(), sp)
+    for _ in range(iters):
+        c.compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay.data_ptr(), cap, d_size.data_ptr(), sp)
     c.sync_status(sp)
     L.myyuv_debug_k2_stamps(st)
-    nw = ((w*h*3//2)//64 + 63)//64 * 10
     ks = c.kernel_stats()
-    print(label, 'huff_encode us', round(ks['huff_encode'][0]/ks['huff_encode'][1]*1e3,1),
-          ' cycles/wave:', {names[k]: round(st[k]/nw) for k in range(1,7)}, flush=True)
+    c.profile(False)
+    nw = ((w * h * 3 // 2) // 64 + 63) // 64 * iters
+    fast = {names[k]: round(st[k] / nw) for k in range(1, 6)}
+    wide_sum = {names[k]: st[k + 8] for k in range(1, 6)}
+    wide_max = {names[k]: st[k + 16] for k in range(1, 6)}
+    us = lambda k: round(ks[k][0] / max(ks[k][1], 1) * 1e3, 1)
+    print(f"{label}: fast {us('huff_encode')} us, wide {us('huff_encode_wide')} us", flush=True)
+    print("   fast cycles/wave", fast, flush=True)
+    print("   wide cycles summed", wide_sum, flush=True)
+    print("   wide cycles max/wave", wide_max, flush=True)
+
+
 g = myyuv_file.YUVFile.load(os.path.join(R, 'tests/golden/chef-with-trumpet-big-DCT-50.myyuv'))
 w, h = g.width, g.height
-raw = c.decompress(g.data, w, h, (50, 50, 50))
+raw = O.decompress(g.data, w, h, tuple(g.params))
 run(raw, w, h, 50, 'chef-big q50')
 run(raw, w, h, 90, 'chef-big q90')
 run(synth.noise_frame(2048, 1024).tobytes(), 2048, 1024, 50, 'noise q50')

@@ -48,15 +48,19 @@
 namespace myyuv_gpu {
 
 #ifdef MYYUV_STAMPS
-// diagnostic build only: per-stage wave cycles, summed over waves
-__device__ unsigned long long g_k2_stamps[8];
-#define STAMP(k)                                                                 \
-  do {                                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-    unsigned long long _t = __builtin_amdgcn_s_memtime();                        \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-    if (threadIdx.x == 0 && (k) > 0) atomicAdd(&g_k2_stamps[(k)], _t - _tprev); \
-    _tprev = _t;                                                                 \
+// diagnostic build only: per-stage wave cycles — [0..7] fast pass summed
+// over waves, [8..15] wide pass summed, [16..23] wide pass max over waves
+__device__ unsigned long long g_k2_stamps[24];
+#define STAMP(k)                                                                     \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();                            \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    if (threadIdx.x == 0 && (k) > 0) {                                               \
+      atomicAdd(&g_k2_stamps[(k) + (CAP > 8 ? 8 : 0)], _t - _tprev);                 \
+      if (CAP > 8) atomicMax(&g_k2_stamps[(k) + 16], _t - _tprev);                   \
+    }                                                                                \
+    _tprev = _t;                                                                     \
   } while (0)
 #else
 #define STAMP(k) \
@@ -270,6 +274,27 @@ struct BitWriter {
   }
 };
 
+// Per-position KC slot of the position's symbol, recorded while the distinct
+// symbols are found so the emitter indexes the code table directly instead of
+// probing the hash table again: kBits bits per position, positions static.
+template <int CAP>
+struct SlotIds {
+  static constexpr int kBits = CAP <= 8 ? 3 : (CAP <= 16 ? 4 : 6);
+  static constexpr int kPer = 32 / kBits;
+  static constexpr int kRegs = (64 + kPer - 1) / kPer;
+  uint32_t r[kRegs];
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (int i = 0; i < kRegs; i++) r[i] = 0;
+  }
+  __device__ __forceinline__ void set(int pos, uint32_t slot) {
+    r[pos / kPer] |= slot << (kBits * (pos % kPer));
+  }
+  __device__ __forceinline__ uint32_t get(int pos) const {
+    return (r[pos / kPer] >> (kBits * (pos % kPer))) & ((1u << kBits) - 1u);
+  }
+};
+
 // The lane's block's coefficients (natural order, word w = coefficients 2w,
 // 2w+1), loaded once into registers: every loop over positions below is
 // unrolled, so sym(i) — the i-th coefficient in zig-zag order — is a static
@@ -316,6 +341,8 @@ __device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefRegs& 
   for (int w = 0; w < Layout<CAP>::kTWords; w++) I.wordAt(Layout<CAP>::kT + w) = 0u;
   int n = 0;
   bool has_zero = false, ovf = false;
+  SlotIds<CAP> ids;
+  ids.clear();
   // Positions are visited with a static index (R.sym(i) must stay a register
   // read), in groups of 8 behind one wave-uniform test of the wave's msz.
 #pragma unroll
@@ -328,6 +355,7 @@ __device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefRegs& 
         if (i < msz && !ovf) {
           has_zero |= (v == 0);
           uint32_t h = thash<CAP>(v);
+          uint32_t slot = 0;
           while (true) {
             const uint32_t e = I.t8(h);
             if (e == 0) {
@@ -336,6 +364,7 @@ __device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefRegs& 
               } else {
                 I.t8(h) = (uint8_t)(n + 1);
                 I.kc(n) = ((uint32_t)v & 0x7FFu) | (1u << 11);
+                slot = (uint32_t)n;
                 n++;
               }
               break;
@@ -343,10 +372,12 @@ __device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefRegs& 
             const uint32_t kw = I.kc(e - 1);
             if (nkey(kw) == v) {
               I.kc(e - 1) = kw + (1u << 11);
+              slot = e - 1;
               break;
             }
             h = (h + 1) & (Layout<CAP>::kTEntries - 1);
           }
+          ids.set(i, slot);
         }
       }
     }
@@ -483,15 +514,8 @@ __device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefRegs& 
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int i = i0 + k;
-        const int v = R.sym(i);
         if (i < msz) {
-          uint32_t h = thash<CAP>(v);
-          uint32_t w;
-          while (true) {
-            w = I.kc(I.t8(h) - 1);
-            if (nkey(w) == v) break;
-            h = (h + 1) & (Layout<CAP>::kTEntries - 1);
-          }
+          const uint32_t w = I.kc((int)ids.get(i));
           bw.put(w >> 22, (int)((w >> 18) & 15u));
         }
       }

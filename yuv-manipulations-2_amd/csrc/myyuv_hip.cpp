@@ -38,7 +38,7 @@ __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const S
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
                               uint4*, unsigned long long*);
 #ifdef MYYUV_STAMPS
-extern __device__ unsigned long long g_k2_stamps[8];
+extern __device__ unsigned long long g_k2_stamps[24];
 #endif
 }  // namespace myyuv_gpu
 
@@ -597,11 +597,11 @@ int myyuv_hip_kernel_stats(myyuv_hip_handle c, double ms[MYYUV_K_COUNT],
 
 // Diagnostic builds (-DMYYUV_STAMPS): summed per-stage wave cycles of K2
 // since the last call; returns MYYUV_E_ARG in normal builds.
-int myyuv_debug_k2_stamps(unsigned long long out[8]) {
+int myyuv_debug_k2_stamps(unsigned long long out[24]) {
 #ifdef MYYUV_STAMPS
-  unsigned long long zero[8] = {0};
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_stamps), 64) != hipSuccess) return MYYUV_E_HIP;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_k2_stamps), zero, 64) != hipSuccess) return MYYUV_E_HIP;
+  unsigned long long zero[24] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_stamps), 192) != hipSuccess) return MYYUV_E_HIP;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_k2_stamps), zero, 192) != hipSuccess) return MYYUV_E_HIP;
   return 0;
 #else
   (void)out;
