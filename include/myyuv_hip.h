@@ -115,9 +115,10 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
 #define MYYUV_K_PARSE 4      /* decode-side stream header parse */
 #define MYYUV_K_HUFF_DEC 5   /* K5 huff_decode */
 #define MYYUV_K_IDCT 6       /* K6 dequant_idct */
-#define MYYUV_K_HUFF_WIDE 7  /* K2 overflow pass (CAP=64, worklist) */
+#define MYYUV_K_HUFF_WIDE 7  /* K2 overflow pass, lane per block (long worklists) */
 #define MYYUV_K_SCAN_SUMS 8  /* scan of chunk sizes, tile-prefix pass */
-#define MYYUV_K_COUNT 9
+#define MYYUV_K_HUFF_WAVE 9  /* K2 overflow pass, wave per block (short worklists) */
+#define MYYUV_K_COUNT 10
 int myyuv_hip_profile(myyuv_hip_handle h, int enable);
 int myyuv_hip_kernel_stats(myyuv_hip_handle h, double ms[MYYUV_K_COUNT],
                            int64_t launches[MYYUV_K_COUNT]);

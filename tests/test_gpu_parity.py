@@ -75,6 +75,19 @@ def test_noise_vs_oracle(codec, oracle, q):
     assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q)
 
 
+@pytest.mark.parametrize("q", [(50, 50, 50), (100, 100, 100)])
+def test_noise_long_overflow_list(codec, oracle, q):
+    """A noise frame whose blocks nearly all exceed 8 distinct symbols: the
+    overflow worklist is longer than kWaveEncodeLimit (24576), so K2 takes the
+    lane-per-block overflow pass instead of the wave-per-block one."""
+    import synth
+    w, h = 2048, 1024  # 49,152 blocks
+    fr = synth.noise_frame(w, h)
+    pay = codec.compress(fr.tobytes(), w, h, q)
+    assert pay == oracle.compress(fr.tobytes(), w, h, q)
+    assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q)
+
+
 @pytest.mark.parametrize("wh", [(16, 16), (48, 16), (16, 48), (1008, 16), (144, 272)])
 def test_odd_geometries(codec, oracle, wh):
     w, h = wh

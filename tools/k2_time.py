@@ -27,7 +27,7 @@ def run(raw, w, h, q, label, iters=10):
     for _ in range(3):
         c.compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay.data_ptr(), cap, d_size.data_ptr(), sp)
     c.sync_status(sp)
-    st = (ctypes.c_ulonglong * 24)()
+    st = (ctypes.c_ulonglong * 40)()
     L.myyuv_debug_k2_stamps(st)
     c.profile(True)
     for _ in range(iters):
@@ -45,6 +45,19 @@ def run(raw, w, h, q, label, iters=10):
     print("   fast cycles/wave", fast, flush=True)
     print("   wide cycles summed", wide_sum, flush=True)
     print("   wide cycles max/wave", wide_max, flush=True)
+    wn = ['', 'load', 'distinct', 'map', 'heap', 'len', 'canon', 'emit']
+    import numpy as np
+    ws = np.zeros(65536 * 8, np.uint32)
+    L.myyuv_debug_k2_wstamps(ws.ctypes.data_as(ctypes.c_void_p), 65536)
+    ws = ws.reshape(-1, 8)[:, 1:]
+    used = ws.sum(1) > 0
+    if used.any():
+        ws = ws[used]
+        tot = ws.sum(1)
+        print(f"   wave encoder {us('huff_encode_wave')} us; {used.sum()} blocks; cycles per block: "
+              f"mean {tot.mean():.0f} p50 {np.median(tot):.0f} p99 {np.percentile(tot, 99):.0f} max {tot.max()}", flush=True)
+        print("   mean per phase", {wn[k + 1]: int(ws[:, k].mean()) for k in range(7)}, flush=True)
+        print("   max per phase", {wn[k + 1]: int(ws[:, k].max()) for k in range(7)}, flush=True)
 
 
 g = myyuv_file.YUVFile.load(os.path.join(R, 'tests/golden/chef-with-trumpet-big-DCT-50.myyuv'))

@@ -84,6 +84,11 @@ constexpr float kNearScale = 2.0f * 1100.0f * 0x1p-21f;
 // scan is a fixed permutation applied with static register indices where the
 // coefficients are consumed (K2) or produced (K5).
 constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
+
+// K2 overflow worklists up to this many blocks are encoded wave-per-block
+// (k_huff_encode_wave), longer ones lane-per-block (k_huff_encode_wide).
+constexpr uint32_t kWaveEncodeLimit = 24576;
+constexpr uint32_t kWaveEncodeGrid = 16384;  // waves of k_huff_encode_wave
 __host__ __device__ __forceinline__ uint32_t coef_quad(uint32_t g, uint32_t c) {
   return ((g >> 6) * 8u + c) * 64u + (g & 63u);
 }

@@ -50,7 +50,7 @@ namespace myyuv_gpu {
 #ifdef MYYUV_STAMPS
 // diagnostic build only: per-stage wave cycles — [0..7] fast pass summed
 // over waves, [8..15] wide pass summed, [16..23] wide pass max over waves
-__device__ unsigned long long g_k2_stamps[24];
+__device__ unsigned long long g_k2_stamps[40];
 #define STAMP(k)                                                                     \
   do {                                                                               \
     __builtin_amdgcn_sched_barrier(0);                                               \
@@ -62,7 +62,22 @@ __device__ unsigned long long g_k2_stamps[24];
     }                                                                                \
     _tprev = _t;                                                                     \
   } while (0)
+// wave encoder: per-block phase cycles into g_k2_wstamps[block slot][8]
+// (plain stores: contended atomics would distort the timing)
+__device__ uint32_t g_k2_wstamps[65536 * 8];
+#define WSTAMP(k)                                                                    \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();                            \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    if (threadIdx.x == 0 && (k) > 0 && _wslot < 65536)                               \
+      g_k2_wstamps[_wslot * 8 + (k)] = (uint32_t)(_t - _wprev);                      \
+    _wprev = _t;                                                                     \
+  } while (0)
 #else
+#define WSTAMP(k) \
+  do {            \
+  } while (0)
 #define STAMP(k) \
   do {           \
   } while (0)
@@ -71,6 +86,7 @@ __device__ unsigned long long g_k2_stamps[24];
 namespace {
 
 constexpr uint32_t kNil = 127;     // next-pointer "null"
+__constant__ uint8_t c_zz_lane[64] = MYYUV_ZIGZAG;
 constexpr uint32_t kEmpty = 0x80;  // bucket has no before-pointer
 constexpr uint32_t kHead = 0x7F;   // before-pointer = list head sentinel
 
@@ -533,7 +549,266 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
+// ---------------------------------------------------------------------------
+// Wave-per-block encoder for short overflow worklists (natural images: a few
+// percent of blocks have more than 8 distinct symbols).  In the lane-per-block
+// pass such a wave is one long chain of dependent LDS round trips (heap
+// merges, insertion sort, map replay), and a few hundred waves leave the chip
+// idle.  Here one wave encodes one block: lanes are the block's positions /
+// distinct symbols / heap slots, every order-independent step is lane
+// parallel (distinct symbols by ballot, map order and canonical order by
+// rank counting, code bits by prefix sum), and the inherently sequential
+// steps (heap merges, depth chain) run as uniform control over
+// lane-distributed arrays: a v_readlane / v_writelane per step instead of an
+// LDS round trip.  Same byte output as encode_block (same libstdc++ replay):
+//   * unordered_map iteration order in closed form: with front-of-bucket /
+//     front-of-list insertion (_M_insert_bucket_begin) the list is the bucket
+//     runs in decreasing order of their first insertion, each run in
+//     decreasing insertion order; a rehash re-inserts the nodes in list order
+//     with the same rule, so every phase is that ordering applied to the
+//     sequence (previous walk order, then the later inserts).
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ uint32_t wl(uint32_t arr, uint32_t val, int lane) {
+  return threadIdx.x == (uint32_t)lane ? val : arr;  // val, lane wave-uniform
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// Walk order of nodes 0..cnt-1 (lane = node) under the insertion rule, for
+// sequence positions q and bucket count `ph`'s: lane's position in the list.
+__device__ __forceinline__ uint32_t map_walk(int key, uint32_t q, int cnt, int ph) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t b = bucket_of(key, phase_of(ph));
+  uint32_t F = q;  // first insertion (min q) of the lane's bucket
+  for (int t = 0; t < cnt; t++) {
+    const uint32_t bt = rl(b, t), qt = rl(q, t);
+    if (bt == b && qt < F) F = qt;
+  }
+  uint32_t rank = 0;
+  for (int t = 0; t < cnt; t++) {
+    const uint32_t Ft = rl(F, t), qt = rl(q, t);
+    rank += (Ft > F || (Ft == F && qt > q)) ? 1u : 0u;
+  }
+  return lane < (uint32_t)cnt ? rank : lane;
+}
+
+__device__ __forceinline__ void wheap_sift_up(uint32_t& heap, int hole, uint32_t e) {
+  while (hole > 0) {
+    const int parent = (hole - 1) >> 1;
+    const uint32_t pe = rl(heap, parent);
+    if ((pe >> 8) <= (e >> 8)) break;
+    heap = wl(heap, pe, hole);
+    hole = parent;
+  }
+  heap = wl(heap, e, hole);
+}
+
+__device__ __forceinline__ uint32_t wheap_pop(uint32_t& heap, int& len) {
+  const uint32_t top = rl(heap, 0);
+  const int m = --len;
+  if (m > 0) {
+    const uint32_t value = rl(heap, m);
+    int hole = 0, child = 0;
+    while (child < (m - 1) / 2) {
+      child = 2 * (child + 1);
+      const uint32_t right = rl(heap, child), left = rl(heap, child - 1);
+      uint32_t pick = right;
+      if ((right >> 8) > (left >> 8)) {
+        child--;
+        pick = left;
+      }
+      heap = wl(heap, pick, hole);
+      hole = child;
+    }
+    if ((m & 1) == 0 && child == (m - 2) / 2) {
+      child = 2 * (child + 1);
+      heap = wl(heap, rl(heap, child - 1), hole);
+      hole = child - 1;
+    }
+    wheap_sift_up(heap, hole, value);
+  }
+  return top;
+}
+
+// OR `nb` bits of `v` at bit offset `off` into the chunk image.
+__device__ __forceinline__ void put_bits(uint32_t* img, uint32_t off, uint32_t v, uint32_t nb) {
+  if (nb == 0) return;
+  const uint32_t w = off >> 5, sh = off & 31u;
+  atomicOr(&img[w], v << sh);
+  if (sh + nb > 32) atomicOr(&img[w + 1], v >> (32 - sh));
+}
+
+__device__ void encode_block_wave(const uint4* __restrict__ coef, uint32_t g, uint32_t* img,
+                                  uint32_t* __restrict__ slots, uint8_t* __restrict__ sizes,
+                                  uint32_t _wslot = 0) {
+  const uint32_t lane = threadIdx.x;
+#ifdef MYYUV_STAMPS
+  unsigned long long _wprev = 0;
+#endif
+  WSTAMP(0);
+  // ---- lane i: zig-zag position i (Huffman.cpp:176-182)
+  const uint32_t nat = c_zz_lane[lane];
+  const uint32_t word =
+      reinterpret_cast<const uint32_t*>(coef)[coef_quad(g, nat >> 3) * 4u + ((nat >> 1) & 3u)];
+  const int v = (int)(int16_t)(word >> (16 * (nat & 1)));
+  const uint64_t nzm = __ballot(v != 0);
+  int msz = nzm ? 64 - __clzll((long long)nzm) : 0;
+  if (msz == 0) msz = 1;  // all-zero block: one symbol 0 (Huffman.cpp:191-194)
+  const bool act = lane < (uint32_t)msz;
+  const bool has_zero = __ballot(act && v == 0) != 0;
+  WSTAMP(1);
+
+  // ---- distinct symbols in first-occurrence order (operator[] insertion
+  // order, Huffman.cpp:183): lane s of key/cnt = symbol s; slot = the
+  // position's symbol
+  uint32_t cntv = 0, slot = 0;
+  int key = 0;
+  int n = 0;
+  for (int j = 0; j < msz; j++) {
+    const int vj = (int)rl((uint32_t)v, j);
+    const uint64_t eq = __ballot(act && v == vj);
+    if ((eq & ((1ull << j) - 1ull)) == 0) {  // first occurrence
+      key = (int)wl((uint32_t)key, (uint32_t)vj, n);
+      cntv = wl(cntv, (uint32_t)__popcll(eq), n);
+      if ((eq >> lane) & 1ull) slot = (uint32_t)n;
+      n++;
+    }
+  }
+  const bool sym = lane < (uint32_t)n;
+  WSTAMP(2);
+
+  // ---- std::unordered_map iteration order (rehash before the 14th, 30th,
+  // 60th insert; the freq[0] probe's rehash, Huffman.cpp:186-197)
+  int ph = 0;
+  uint32_t q = lane;
+  const int nbs[4] = {13, 29, 59, 127};
+  while (n > nbs[ph]) {
+    q = map_walk(key, q, nbs[ph], ph);
+    ph++;
+  }
+  if (!has_zero && n == nbs[ph]) {
+    q = map_walk(key, q, n, ph);
+    ph++;
+  }
+  const uint32_t order = map_walk(key, q, n, ph);  // lane s: list position of symbol s
+  WSTAMP(3);
+
+  // ---- Huffman merges on a lane-distributed heap (libstdc++ push/pop_heap)
+  uint32_t heap = 0, lpar = 0, ipar = 0;
+  int hlen = 0;
+  for (int r = 0; r < n; r++) {
+    const int node = __ffsll((long long)__ballot(sym && order == (uint32_t)r)) - 1;
+    wheap_sift_up(heap, hlen++, (rl(cntv, node) << 8) | (uint32_t)node);
+  }
+  for (int k = 0; k + 1 < n; k++) {
+    const uint32_t l = wheap_pop(heap, hlen);
+    const uint32_t r = wheap_pop(heap, hlen);
+    const uint32_t li = l & 0xFF, ri = r & 0xFF;
+    if (li < 64) lpar = wl(lpar, (uint32_t)k, (int)li);
+    else ipar = wl(ipar, (uint32_t)k, (int)(li - 64));
+    if (ri < 64) lpar = wl(lpar, (uint32_t)k, (int)ri);
+    else ipar = wl(ipar, (uint32_t)k, (int)(ri - 64));
+    wheap_sift_up(heap, hlen++, (((l >> 8) + (r >> 8)) << 8) | (uint32_t)(64 + k));
+  }
+  WSTAMP(4);
+  // ---- code lengths (generateCodeLength, Huffman.cpp:71-83): depth chain
+  uint32_t len = 1;
+  if (n >= 2) {
+    uint32_t dep = wl(0u, 0u, n - 2);  // root = last internal node
+    for (int k = n - 3; k >= 0; k--) dep = wl(dep, rl(dep, (int)rl(ipar, k)) + 1u, k);
+    len = (uint32_t)__shfl((int)dep, (int)lpar, 64) + 1u;
+  }
+  const uint32_t nbits = wave_sum(sym ? cntv * len : 0u);
+  uint32_t cl[9];
+#pragma unroll
+  for (int l = 1; l <= 8; l++) cl[l] = (uint32_t)__popcll(__ballot(sym && len == (uint32_t)l));
+
+  WSTAMP(5);
+  // ---- canonical order (length, symbol) and codes (generateCanonicalTree,
+  // Huffman.cpp:86-103): rank by counting; first code / first rank per length
+  const uint32_t ckey = (len << 11) | (uint32_t)(key + 1024);
+  uint32_t crank = 0;
+  for (int t = 0; t < n; t++) crank += rl(ckey, t) < ckey ? 1u : 0u;
+  uint32_t fc = 0, fr = 0, myfc = 0, myfr = 0, gbase = 3, mygb = 0;
+  uint32_t table_bytes = 0;
+#pragma unroll
+  for (int l = 1; l <= 8; l++) {
+    if (len == (uint32_t)l) {
+      myfc = fc;
+      myfr = fr;
+      mygb = gbase;
+    }
+    const uint32_t c = cl[l];
+    const uint32_t gb = c > 32 ? 2 + 44 + ((c - 32) * 11 + 7) / 8 : (c ? 1 + (c * 11 + 7) / 8 : 0);
+    gbase += gb;
+    table_bytes += gb;
+    fc = (fc + c) << 1;
+    fr += c;
+  }
+  const uint32_t code = myfc + (crank - myfr);
+  const uint32_t rcode = __brev(code) >> (32 - len);
+
+  WSTAMP(6);
+  // ---- chunk image (Huffman::dump, Huffman.cpp:279-326), LSB-first
+  if (lane < (uint32_t)kSlotWords) img[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    atomicOr(&img[0], nbits | (table_bytes << 16));
+    uint32_t b = 3;
+#pragma unroll
+    for (int l = 1; l <= 8; l++) {
+      const uint32_t c = cl[l];
+      if (c) {
+        put_bits(img, 8 * b, ((uint32_t)(l - 1) << 5) | ((c > 32 ? 32 : c) - 1), 8);
+        if (c > 32) put_bits(img, 8 * (b + 45), ((uint32_t)(l - 1) << 5) | (c - 33), 8);
+        b += c > 32 ? 2 + 44 + ((c - 32) * 11 + 7) / 8 : 1 + (c * 11 + 7) / 8;
+      }
+    }
+  }
+  if (sym) {  // 11-bit values in canonical order (pack11bit)
+    const uint32_t j = crank - myfr;
+    const uint32_t off = j < 32 ? 8 * (mygb + 1) + 11 * j : 8 * (mygb + 46) + 11 * (j - 32);
+    put_bits(img, off, (uint32_t)key & 0x7FFu, 11);
+  }
+  // code bits of the message, position order
+  const uint32_t pl = act ? (uint32_t)__shfl((int)len, (int)slot, 64) : 0u;
+  const uint32_t pc = (uint32_t)__shfl((int)rcode, (int)slot, 64);
+  uint32_t pre = pl;  // inclusive prefix sum over lanes
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)pre, d, 64);
+    if (lane >= (uint32_t)d) pre += o;
+  }
+  if (act) put_bits(img, 8 * (3 + table_bytes) + pre - pl, pc, pl);
+  __builtin_amdgcn_wave_barrier();
+  if (lane < (uint32_t)kSlotWords)
+    slots[(size_t)(g >> 6) * (kSlotWords * kWave) + lane * kWave + (g & 63)] = img[lane];
+  if (lane == 0) sizes[g] = (uint8_t)(3 + table_bytes + (nbits + 7) / 8);
+  WSTAMP(7);
+}
+
 }  // namespace
+
+// Overflow pass for short worklists: one wave per listed block (see
+// encode_block_wave); exits at once when the list is long (the lane pass
+// k_huff_encode_wide takes it).
+__global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict__ coef,
+                                                        uint32_t* __restrict__ slots,
+                                                        uint8_t* __restrict__ sizes,
+                                                        const uint32_t* __restrict__ work,
+                                                        const uint32_t* __restrict__ work_count) {
+  __shared__ uint32_t img[kSlotWords + 2];
+  const uint32_t cnt = *work_count;
+  if (cnt > kWaveEncodeLimit) return;
+  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) encode_block_wave(coef, work[i], img, slots, sizes, i);
+}
 
 // Fast pass over every block (CAP=8); blocks with more distinct symbols are
 // appended to `work` for k_huff_encode_wide.
@@ -568,8 +843,10 @@ __global__ __launch_bounds__(64) void k_huff_encode(const uint4* __restrict__ co
   }
 }
 
-// Overflow pass (CAP=64): the blocks listed in `work` (count in *work_count),
-// 64 per workgroup; the grid is sized for the worst case, idle groups exit.
+// Overflow pass (CAP=64), lane per block, for long worklists (noise-like
+// frames where most blocks overflow): the blocks listed in `work` (count in
+// *work_count), 64 per workgroup; the grid is sized for the worst case, idle
+// groups exit.  Short lists go to k_huff_encode_wave instead.
 __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict__ coef,
                                                         uint32_t* __restrict__ slots,
                                                         uint8_t* __restrict__ sizes,
@@ -579,7 +856,7 @@ __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict
   __shared__ uint32_t lds[Layout<CAP>::kWords * kWave];
   const uint32_t cnt = *work_count;
   const uint32_t i = blockIdx.x * kWave + threadIdx.x;
-  if (blockIdx.x * kWave >= cnt) return;
+  if (cnt <= kWaveEncodeLimit || blockIdx.x * kWave >= cnt) return;  // small lists: k_huff_encode_wave
   const bool live = i < cnt;
   const uint32_t g = live ? work[i] : 0;
   CoefRegs R;

@@ -25,6 +25,8 @@ __global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*);
 __global__ void k_dequant_idct(const uint4*, FrameGeom, const QTables*, uint8_t*);
 __global__ void k_huff_encode(const uint4*, uint32_t, uint32_t*, uint8_t*,
                               uint32_t*, uint32_t*);
+__global__ void k_huff_encode_wave(const uint4*, uint32_t*, uint8_t*, const uint32_t*,
+                                   const uint32_t*);
 __global__ void k_huff_encode_wide(const uint4*, uint32_t*, uint8_t*,
                                    const uint32_t*, const uint32_t*);
 __global__ void k_scan_tiles(const uint8_t*, ScanSrc, const StreamDesc*, uint32_t*, uint32_t*);
@@ -38,7 +40,8 @@ __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const S
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
                               uint4*, unsigned long long*);
 #ifdef MYYUV_STAMPS
-extern __device__ unsigned long long g_k2_stamps[24];
+extern __device__ unsigned long long g_k2_stamps[40];
+extern __device__ uint32_t g_k2_wstamps[65536 * 8];
 #endif
 }  // namespace myyuv_gpu
 
@@ -250,8 +253,10 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   return e ? MYYUV_E_HIP : 0;
 }
 
-// K2: fast pass over all blocks, then the wide pass over the blocks with more
-// than 16 distinct symbols (worklist filled on the device; no host sync).
+// K2: fast pass over all blocks, then the overflow pass over the blocks with
+// more than 8 distinct symbols (worklist filled on the device; no host sync):
+// wave-per-block for short lists, lane-per-block for long ones — both
+// kernels are queued and each returns at once outside its regime.
 int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, hipStream_t s) {
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
@@ -259,6 +264,9 @@ int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, hipStream_t s) {
   int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(ceil_div(nblk, kWave)), dim3(kWave), s,
                  c->coef.as<const uint4>(), nblk, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
                  list, count);
+  e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
+              c->coef.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
+              (const uint32_t*)list, (const uint32_t*)count);
   e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(ceil_div(nblk, kWave)), dim3(kWave), s,
               c->coef.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
               (const uint32_t*)list, (const uint32_t*)count);
@@ -595,13 +603,25 @@ int myyuv_hip_kernel_stats(myyuv_hip_handle c, double ms[MYYUV_K_COUNT],
   return 0;
 }
 
+// Diagnostic builds: per-block phase cycles of the wave encoder (n blocks).
+int myyuv_debug_k2_wstamps(uint32_t* out, uint32_t n) {
+#ifdef MYYUV_STAMPS
+  if (n > 65536) n = 65536;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_wstamps), (size_t)n * 32) == hipSuccess ? 0 : MYYUV_E_HIP;
+#else
+  (void)out;
+  (void)n;
+  return MYYUV_E_ARG;
+#endif
+}
+
 // Diagnostic builds (-DMYYUV_STAMPS): summed per-stage wave cycles of K2
 // since the last call; returns MYYUV_E_ARG in normal builds.
-int myyuv_debug_k2_stamps(unsigned long long out[24]) {
+int myyuv_debug_k2_stamps(unsigned long long out[40]) {
 #ifdef MYYUV_STAMPS
-  unsigned long long zero[24] = {0};
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_stamps), 192) != hipSuccess) return MYYUV_E_HIP;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_k2_stamps), zero, 192) != hipSuccess) return MYYUV_E_HIP;
+  unsigned long long zero[40] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_stamps), 320) != hipSuccess) return MYYUV_E_HIP;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_k2_stamps), zero, 320) != hipSuccess) return MYYUV_E_HIP;
   return 0;
 #else
   (void)out;

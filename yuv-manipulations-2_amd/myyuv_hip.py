@@ -19,9 +19,9 @@ E_DCTYUV_SIZE, E_PLANE_SIZE, E_PLANE_NBLK, E_PLANE_CONTENT = 6, 7, 8, 9
 E_BAD_CODE, E_UNKNOWN_SYMBOL, E_BAD_CHUNK, E_HIP, E_NO_DEVICE = 10, 11, 12, 13, 14
 
 KERNELS = ["fdct_quant", "huff_encode", "scan_tiles", "compact", "parse", "huff_decode",
-           "dequant_idct", "huff_encode_wide", "scan_sums"]
+           "dequant_idct", "huff_encode_wide", "scan_sums", "huff_encode_wave"]
 (K_FDCT, K_HUFF_ENC, K_SCAN, K_COMPACT, K_PARSE, K_HUFF_DEC, K_IDCT, K_HUFF_WIDE,
- K_SCAN_SUMS) = range(9)
+ K_SCAN_SUMS, K_HUFF_WAVE) = range(10)
 
 # the exported symbols include/myyuv_hip.h declares (checked by the CPU tests)
 EXPORTS = [
