@@ -120,6 +120,10 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
 #define MYYUV_K_HUFF_WAVE 9  /* K2 overflow pass, wave per block (short worklists) */
 #define MYYUV_K_COUNT 10
 int myyuv_hip_profile(myyuv_hip_handle h, int enable);
+/* As myyuv_hip_profile, but stamps only the kernels whose bit (1 << MYYUV_K_*)
+ * is set in `mask` (0 disables): event stamping costs host and queue time per
+ * launch, so a timed region profiles just the kernel it reports on. */
+int myyuv_hip_profile_kernels(myyuv_hip_handle h, uint32_t mask);
 int myyuv_hip_kernel_stats(myyuv_hip_handle h, double ms[MYYUV_K_COUNT],
                            int64_t launches[MYYUV_K_COUNT]);
 

@@ -147,7 +147,7 @@ struct myyuv_hip_ctx {
   uint8_t q_cached[3] = {0, 0, 0};
   bool q_valid = false;
   // profiling
-  bool prof = false;
+  uint32_t prof = 0;  // bit k: stamp kernel id k
   double ms[MYYUV_K_COUNT] = {};
   int64_t launches[MYYUV_K_COUNT] = {};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -188,7 +188,8 @@ template <class... KArgs, class... Args>
 int launch(myyuv_hip_ctx* c, int kid, void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t s,
            Args... args) {
   hipEvent_t a = nullptr, b = nullptr;
-  if (c->prof) {
+  const bool stamp = (c->prof >> kid) & 1u;
+  if (stamp) {
     a = take_event(c);
     b = take_event(c);
   }
@@ -197,7 +198,7 @@ int launch(myyuv_hip_ctx* c, int kid, void (*k)(KArgs...), dim3 grid, dim3 block
     (void)hipGetLastError();
     return MYYUV_E_HIP;
   }
-  if (c->prof) c->pending.push_back({kid, {a, b}});
+  if (stamp) c->pending.push_back({kid, {a, b}});
   return 0;
 }
 
@@ -577,12 +578,16 @@ int myyuv_gpu_dct_decompress(myyuv_hip_handle c, const uint8_t* payload, uint32_
 }
 
 int myyuv_hip_profile(myyuv_hip_handle c, int enable) {
+  return myyuv_hip_profile_kernels(c, enable ? (1u << MYYUV_K_COUNT) - 1u : 0u);
+}
+
+int myyuv_hip_profile_kernels(myyuv_hip_handle c, uint32_t mask) {
   if (!c) return MYYUV_E_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   (void)hipStreamSynchronize(c->stream);
   drain_profile(c);
-  c->prof = enable != 0;
+  c->prof = mask & ((1u << MYYUV_K_COUNT) - 1u);
   for (int k = 0; k < MYYUV_K_COUNT; k++) {
     c->ms[k] = 0;
     c->launches[k] = 0;

@@ -28,7 +28,7 @@ EXPORTS = [
     "myyuv_hip_create", "myyuv_hip_destroy", "myyuv_hip_strerror", "myyuv_dct_payload_bound",
     "myyuv_gpu_dct_compress", "myyuv_gpu_dct_decompress", "myyuv_hip_reserve",
     "myyuv_gpu_dct_compress_device", "myyuv_gpu_dct_decompress_device", "myyuv_hip_sync_status",
-    "myyuv_hip_profile", "myyuv_hip_kernel_stats", "myyuv_gpu_fdct_blocks",
+    "myyuv_hip_profile", "myyuv_hip_profile_kernels", "myyuv_hip_kernel_stats", "myyuv_gpu_fdct_blocks",
     "myyuv_gpu_huff_encode_blocks",
 ]
 
@@ -85,6 +85,7 @@ def load():
     L.myyuv_gpu_dct_decompress_device.argtypes = [vp, vp, vp, u32, u32, u32, u8p, vp, vp]
     L.myyuv_hip_sync_status.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int64)]
     L.myyuv_hip_profile.argtypes = [vp, ctypes.c_int]
+    L.myyuv_hip_profile_kernels.argtypes = [vp, ctypes.c_uint32]
     L.myyuv_hip_kernel_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_int64)]
     L.myyuv_gpu_fdct_blocks.argtypes = [vp, u8p, u32, ctypes.POINTER(ctypes.c_float),
@@ -183,8 +184,13 @@ class Codec:
         rc = load().myyuv_hip_sync_status(self._h, stream, ctypes.byref(bad))
         return rc, bad.value
 
-    def profile(self, enable):
-        rc = load().myyuv_hip_profile(self._h, 1 if enable else 0)
+    def profile(self, enable, kernels=None):
+        """Per-kernel event stamping: all kernels, or only the named ones."""
+        if kernels is None:
+            rc = load().myyuv_hip_profile(self._h, 1 if enable else 0)
+        else:
+            mask = sum(1 << KERNELS.index(k) for k in kernels) if enable else 0
+            rc = load().myyuv_hip_profile_kernels(self._h, mask)
         if rc:
             raise CodecError(rc)
 
