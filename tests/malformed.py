@@ -45,6 +45,56 @@ def _unknown_symbol(chunk, s):
     return bytes([nbits & 0xFF, nbits >> 8]) + body
 
 
+def _pack11(vals):
+    acc = 0
+    for i, v in enumerate(vals):
+        acc |= (v & 0x7FF) << (11 * i)
+    return acc.to_bytes((11 * len(vals) + 7) // 8, "little")
+
+
+def _irregular_chunk(groups, seq, s):
+    """A valid chunk whose table is not what the reference encoder writes.
+    groups: [(length, [values...]), ...] in stream order (a length may recur:
+    Huffman::fromDump appends); seq: values to emit.  Codes follow the
+    decoder's rule: length-L codes start at first_L, in append order."""
+    by_len = {}
+    for L, vals in groups:
+        by_len.setdefault(L, []).extend(vals)
+    code_of, first = {}, 0
+    for L in range(1, 9):
+        for k, v in enumerate(by_len.get(L, [])):
+            code_of.setdefault(v, (L, first + k))
+        first = (first + len(by_len.get(L, []))) << 1
+    table = b"".join(bytes([((L - 1) << 5) | (len(v) - 1)]) + _pack11(v) for L, v in groups)
+    bits, nbits = 0, 0
+    for v in seq:
+        L, code = code_of[v]
+        for b in range(L - 1, -1, -1):  # MSB-first into an LSB-first stream
+            bits |= ((code >> b) & 1) << nbits
+            nbits += 1
+    body = bytes([nbits & 0xFF, nbits >> 8, len(table)]) + table + \
+        bits.to_bytes((nbits + 7) // 8, "little")
+    assert len(body) <= s, (len(body), s)
+    return body + bytes(s - len(body))
+
+
+def irregular_cases(payload):
+    """(name, payload) of VALID streams with tables outside the encoder's
+    form: lengths out of order and split across groups; more than 32 codes of
+    one length (two groups).  The decode must match the oracle exactly."""
+    g1 = [(3, [-7]), (1, [0]), (3, [1023]), (2, [-1024])]
+    seq1 = [0, -7, 1023, 0, -1024, 0, 0, -7, -1024, 1023] * 3
+    vals = list(range(-20, 21))  # 41 distinct
+    g2 = [(2, [vals[0]]), (7, vals[1:33]), (7, vals[33:])]
+    seq2 = vals[:64] + vals[:23]
+    out = []
+    for name, g, seq in (("split_out_of_order", g1, seq1), ("over_32_per_length", g2, seq2)):
+        need = len(_irregular_chunk(g, seq, 4096).rstrip(b"\0")) + 1
+        out.append((name, _replace_chunk(payload, lambda c, s, g=g, q=seq: _irregular_chunk(g, q, s),
+                                         min_size=need)))
+    return out
+
+
 def cases(payload):
     """(name, payload, kind) with kind 'defined' or 'strict'."""
     data = bytearray(payload)

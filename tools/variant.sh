@@ -1,0 +1,16 @@
+#!/bin/bash
+# Diagnostic builds: tools/variant.sh <out-dir> <kernel-file-stem> [hipcc flags...]
+# recompiles csrc/<stem>.hip with the extra flags (e.g. -DMYYUV_K5_EXP=1) and
+# links libmyyuv_hip.so into <out-dir> with the default objects for the rest.
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+P=$R/yuv-manipulations-2_amd
+OUT=$1; STEM=$2; shift 2
+mkdir -p "$OUT"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -I$P/csrc -I$R/include"
+/opt/rocm/bin/hipcc $FLAGS "$@" -fgpu-rdc -c "$P/csrc/$STEM.hip" -o "$OUT/$STEM.o"
+OBJS="$OUT/$STEM.o"
+for k in k_transform k_huff_encode k_huff_decode k_stream myyuv_hip; do
+  [ "$k" = "$STEM" ] || OBJS="$OBJS $P/build/$k.o"
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -fgpu-rdc --hip-link -shared -o "$OUT/libmyyuv_hip.so" $OBJS

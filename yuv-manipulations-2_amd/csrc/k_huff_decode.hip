@@ -4,23 +4,35 @@
 //
 // One workgroup = one wave = up to 64 consecutive blocks of ONE plane, so the
 // wave's chunks are one contiguous byte range of the plane's content[]; it is
-// staged into LDS with dword loads (the LDS image keeps the stream's dword
-// grid), then each lane decodes its own block:
+// staged into LDS with 16-B loads issued together (the LDS image keeps the
+// stream's 16-B grid; several rounds when it exceeds the 6 KiB stage), then
+// each lane decodes its own block:
 //   1. header: u16 nbits, u8 table_bytes;
-//   2. table: groups ((L-1)<<5 | (n-1)) + n x 11-bit values; two passes so a
-//      length's groups land together however they are ordered (std::map
-//      semantics of tree_data);
+//   2. table: one pass over the groups ((L-1)<<5 | (n-1)) + n x 11-bit values,
+//      recording per length the code count and the bit address of its group.
+//      No symbol table is unpacked: a decoded code's value is read in place
+//      (11 bits at group_bit + 11 * rank), so the wave needs no LDS beyond
+//      the stage;
 //   3. symbols: the reference decodes bit-serially (puff style): at length L,
 //      code = first L bits, match if code < first + count[L].  Here the next 8
-//      bits are peeked once and the same test is evaluated for L = 1..8
-//      (unrolled, branch-free); the smallest matching L is exactly the length
-//      the bit-serial loop would stop at, including on malformed tables
-//      (uint8 arithmetic of `first` kept), and the bit budget checks give the
-//      same "bad code" / "unknown symbol" outcomes.
-// Output: 64 int16 per block, zero-filled after the last symbol, decoded in
-// zig-zag order into LDS and written out in natural order (the inverse scan
-// is a compile-time permutation of registers) in the quad layout of
-// codec_common.hpp that K6 reads.
+//      bits are peeked from a 64-bit register window (refilled from LDS every
+//      7 symbols, at most 56 bits apart) and:
+//        * "regular" tables (every length in one group, first + count[L] <=
+//          2^L: every table the reference writes) — the match conditions are
+//          w8 < lim[L] with left-justified limits lim[L] = (first + count) <<
+//          (8 - L), non-decreasing in L, so the matched length is 1 + #{L :
+//          w8 >= lim[L]}: eight 16-bit compares in four SWAR subtractions;
+//        * any other table (malformed or hand-made streams) — the bit-serial
+//          conditions evaluated for L = 1..8 as the reference does (uint8
+//          arithmetic of `first` kept), the value found by walking the groups
+//          of that length in stream order (std::map<len, vector> append
+//          semantics of tree_data).
+//      Both give the reference's "bad code" / "unknown symbol" outcomes on
+//      the same bit budget checks.
+//   The symbol loop is unrolled over the 64 scan positions, so each decoded
+//   value lands in a statically indexed register of the block's NATURAL-order
+//   words (the de-zig-zag of Huffman.cpp:148-153 is free) and the block is
+//   written as 8 quads of the codec_common.hpp layout that K6 reads.
 #include "codec_common.hpp"
 #include "k_stream.hpp"
 
@@ -28,135 +40,242 @@ namespace myyuv_gpu {
 
 namespace {
 
-constexpr int kStageWords = (kWave * kMaxChunk) / 4 + 4;
-constexpr int kOutStride = 65;  // words; conflict-free for both access directions
+// 6 KiB stage: 96 B of chunk per block on average (a 4K frame at q=50 uses
+// ~12 B); a wave whose chunks do not fit is staged in several rounds.
+constexpr uint32_t kStageQuads = 384;
 
-// inverse zig-zag: c_izz[n] = position of natural index n in the scan
-struct IzzTable {
+// diagnostic ablations (never the product): 1 = no symbol decode, 2 = no
+// table parse either
+#ifndef MYYUV_K5_EXP
+#define MYYUV_K5_EXP 0
+#endif
+#ifndef MYYUV_K5_WAVES
+#define MYYUV_K5_WAVES 5
+#endif
+
+
+struct ZzTable {
   uint8_t v[64];
-  constexpr IzzTable() : v{} {
+  constexpr ZzTable() : v{} {
     constexpr uint8_t zz[64] = MYYUV_ZIGZAG;
-    for (int z = 0; z < 64; z++) v[zz[z]] = (uint8_t)z;
+    for (int i = 0; i < 64; i++) v[i] = zz[i];
   }
 };
-constexpr IzzTable kIzz{};
-constexpr const uint8_t* c_izz = kIzz.v;
+constexpr ZzTable kZz{};
+constexpr const uint8_t* c_zz = kZz.v;
+__constant__ uint8_t c_zz_dev[64] = MYYUV_ZIGZAG;
 
 __device__ __forceinline__ void record_error(unsigned long long* err, uint64_t key, int code) {
   atomicMin(err, (unsigned long long)((key << 8) | (uint64_t)code));
 }
 
-// Byte sources for one lane's chunk: the LDS stage (normal case) or global
-// memory (a wave whose chunks do not fit the stage: only malformed streams
-// with oversized chunk_size bytes, up to 255 B each).
-struct LdsBytes {
-  const uint8_t* p;
-  __device__ __forceinline__ uint32_t operator[](uint32_t i) const { return p[i]; }
-};
-struct GlobalBytes {
-  const uint8_t* in;
-  uint32_t base, limit;
-  __device__ __forceinline__ uint32_t operator[](uint32_t i) const {
-    return base + i < limit ? in[base + i] : 0u;
+__device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uint32_t* tile_pre,
+                                            uint32_t g) {
+  return local_off[g] + tile_pre[g / kScanTile];
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
+}
+
+// One lane's chunk in the LDS stage (b0: its first byte).  Bits are in the
+// stream's order: bit k of the chunk is bit k & 7 of byte k >> 3.
+struct LdsChunk {
+  const uint32_t* st;
+  uint32_t b0;
+  __device__ __forceinline__ uint32_t byte(uint32_t i) const {
+    return reinterpret_cast<const uint8_t*>(st)[b0 + i];
+  }
+  __device__ __forceinline__ uint32_t bits32(uint32_t bit) const {
+    const uint32_t P = 8 * b0 + bit, w = P >> 5;
+    return funnel(st[w + 1], st[w], P);
   }
 };
 
-// Returns 0 or the MYYUV_E_* code of the first failure (Huffman::fromDump).
-template <class Bytes, class SymAt, class OutAt>
-__device__ int decode_chunk(const Bytes c, const uint32_t s, SymAt&& sym_at, OutAt&& out_at) {
+struct Table {
+  uint32_t nbits = 0;   // symbol bits
+  uint32_t sbit = 0;    // chunk bit of the first symbol bit
+  uint32_t tb = 0;      // table bytes
+  uint64_t cnt = 0;     // code count of length L in byte L-1
+  uint32_t lim[4] = {0, 0, 0, 0};   // 16-bit fields: left-justified limit, lengths 2k+1, 2k+2
+  uint32_t gpos[4] = {0, 0, 0, 0};  // 16-bit fields: 4096 + group bit - 11 * first
+  bool regular = true;
+};
+
+// Header + table (Huffman::fromDump, Huffman.cpp:243-277).  Returns 0 or the
+// MYYUV_E_* code (12: bad chunk).
+template <class Chunk>
+__device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T) {
+  if (s < 3) return 12;
+  const uint32_t nbits = c.byte(0) | (c.byte(1) << 8);
+  const uint32_t tb = c.byte(2);
+  if (nbits > 512 || 3 + tb + (nbits + 7) / 8 > s) return 12;
+  uint64_t cnt = 0, glo = 0, ghi = 0;
+  uint32_t seen = 0, total = 0, i = 3;
+  bool regular = true;
+  while (i - 3 < tb) {
+    const uint32_t info = c.byte(i);
+    const uint32_t L = (info >> 5) + 1, n = (info & 31) + 1;
+    const uint32_t nbytes = (n * 11 + 7) / 8;
+    total += n;
+    if (i + 1 + nbytes > 3 + tb || total > 64) return 12;
+    cnt += (uint64_t)n << (8 * (L - 1));
+    if (seen & (1u << L)) regular = false;
+    seen |= 1u << L;
+    const uint64_t gb = (uint64_t)(8 * (i + 1)) << (16 * ((L - 1) & 3));
+    if (L <= 4) glo |= gb; else ghi |= gb;
+    i += 1 + nbytes;
+  }
+  uint32_t F = 0;
+#pragma unroll
+  for (int L = 0; L < 8; L++) {  // length L + 1
+    const uint32_t cL = (uint32_t)(cnt >> (8 * L)) & 0xFF;
+    if (F + cL > (2u << L)) regular = false;
+    const uint32_t lim = ((F + cL) << (7 - L)) & 0xFFFF;
+    const uint32_t gb = (uint32_t)((L < 4 ? glo : ghi) >> (16 * (L & 3))) & 0xFFFF;
+    const uint32_t gp = (4096 + gb - 11 * F) & 0xFFFF;
+    T.lim[L >> 1] |= lim << (16 * (L & 1));
+    T.gpos[L >> 1] |= gp << (16 * (L & 1));
+    F = (F + cL) << 1;
+  }
+  T.nbits = nbits;
+  T.sbit = 8 * (3 + tb);
+  T.tb = tb;
+  T.cnt = cnt;
+  T.regular = regular;
+  return 0;
+}
+
+// Value of scan position j into the natural-order words (unpack11bit: 11-bit
+// two's complement, Huffman.cpp:54-69; de-zig-zag, :148-153).
+__device__ __forceinline__ void put_value(uint32_t (&nw)[32], int j, uint32_t raw, bool take) {
+  const uint32_t v = take ? (uint32_t)(((int32_t)(raw << 21)) >> 21) : 0u;
+  const int z = c_zz[j];
+  if (z & 1) nw[z >> 1] |= v << 16;
+  else nw[z >> 1] |= v & 0xFFFFu;
+}
+
+// Symbols of REGULAR tables (Huffman.cpp:106-154) into nw (natural-order
+// int16 pairs, zeroed by the caller).  Returns 0 or the MYYUV_E_* code (10
+// bad code, 11 unknown symbol) for lanes with `act`.
+//
+// Fully unrolled over the 64 scan positions (each value lands in a statically
+// indexed register) in groups of 8 with one uniform "any lane left" test per
+// group; inside a group the body is straight-line (state updates by select:
+// divergent branches, or an exit per position, make the compiler shuffle the
+// whole nw[] array at every join).  The 64-bit window is rebuilt every 7
+// positions (at most 56 bits consumed) from three stage words.
+// (Prefetching those words a few positions ahead, or deferring each value
+// read by one position, measured no faster on MI355X, and with the loads
+// three positions ahead the decoded values came out wrong nondeterministically
+// in long straight-line groups: both are deliberately not done.)
+__device__ __forceinline__ int decode_regular(const LdsChunk& c, const Table& T, bool act,
+                                              uint32_t (&nw)[32]) {
   int code = 0;
-  if (s < 3) {
-    code = 12;
-  } else {
-    const uint32_t nbits = (uint32_t)c[0] | ((uint32_t)c[1] << 8);
-    const uint32_t tb = c[2];
-    if (nbits > 512 || 3 + tb + (nbits + 7) / 8 > s) {
-      code = 12;
-    } else {
-      // pass 1: per-length counts (8 x u8 packed)
-      uint64_t cnt = 0;
-      uint32_t total = 0;
-      uint32_t i = 3;
-      while (i - 3 < tb) {
-        const uint32_t info = c[i];
-        const uint32_t L = (info >> 5) + 1, n = (info & 31) + 1;
-        const uint32_t nbytes = (n * 11 + 7) / 8;
-        total += n;
-        if (i + 1 + nbytes > 3 + tb || total > 64) {
-          code = 12;
+  uint32_t bp = 0, o = 0;
+  uint64_t rwin = 0;  // MSB-first window: chunk bit sbit + bp - o at bit 63
+  act = act && T.nbits > 0;
+  const uint32_t P0 = 8 * c.b0 + T.sbit;  // stage bit of the first symbol bit
+#pragma unroll
+  for (int j0 = 0; j0 < 64; j0 += 8) {
+    if (__ballot(act) == 0) continue;
+#pragma unroll
+    for (int j = j0; j < j0 + 8; j++) {
+      if (j % 7 == 0) {
+        const uint32_t P = P0 + bp, w = P >> 5;
+        const uint32_t q0 = c.st[w], q1 = c.st[w + 1], q2 = c.st[w + 2];
+        rwin = ((uint64_t)__brev(funnel(q1, q0, P)) << 32) | __brev(funnel(q2, q1, P));
+        o = 0;
+      }
+      const uint32_t w8 = (uint32_t)((rwin << o) >> 56);  // next 8 bits, MSB-first
+      // matched length - 1 = #{L : w8 >= lim[L]} (eight 16-bit fields)
+      const uint32_t t = w8 | 0x8000u, W = (t << 16) | t;
+      const uint32_t n = __popc((W - T.lim[0]) & 0x80008000u) +
+                         __popc((W - T.lim[1]) & 0x80008000u) +
+                         __popc((W - T.lim[2]) & 0x80008000u) +
+                         __popc((W - T.lim[3]) & 0x80008000u);
+      const uint32_t L = n + 1;
+      const bool nomatch = n == 8;
+      const bool fail = act && (nomatch || bp + L > T.nbits);
+      code = fail ? (nomatch && bp + 8 <= T.nbits ? 11 : 10) : code;
+      const bool take = act && !fail;
+      const uint64_t gsrc = (n & 4) ? (((uint64_t)T.gpos[3] << 32) | T.gpos[2])
+                                    : (((uint64_t)T.gpos[1] << 32) | T.gpos[0]);
+      const uint32_t G = (uint32_t)(gsrc >> (16 * (n & 3))) & 0xFFFF;
+      const uint32_t vbit = (w8 >> ((7 - n) & 7)) * 11 + G - 4096;  // group bit + 11 * rank
+      put_value(nw, j, c.bits32(take ? vbit : 0u), take);
+      bp = take ? bp + L : bp;
+      o = take ? o + L : o;
+      act = take && bp < T.nbits;
+    }
+  }
+  return code;
+}
+
+// Symbols of any table, bit-serial conditions as the reference evaluates them
+// (uint8 arithmetic of `first` kept), values found by walking the groups of
+// the matched length in stream order; int16 stores straight into the quad
+// layout (slot `g`), zeros after the last symbol.  Only lanes whose table is
+// not regular (malformed or hand-made streams) come here, after the wave's
+// regular lanes, with the unrolled state dead.
+__device__ __forceinline__ int decode_general(const LdsChunk c, const Table T, uint4* coef,
+                                           uint32_t g) {
+  uint16_t* out = reinterpret_cast<uint16_t*>(coef);
+  int code = 0;
+  uint32_t bp = 0, j = 0;
+  while (bp < T.nbits && j < 64) {
+    const uint32_t P = T.sbit + bp;
+    const uint32_t x = c.byte(P >> 3) | (c.byte((P >> 3) + 1) << 8);
+    const uint32_t w8 = __brev((x >> (P & 7)) & 0xFF) >> 24;  // next 8 bits, MSB-first
+    uint32_t first = 0, mL = 0, r = 0;
+    bool neg = false;
+#pragma unroll
+    for (uint32_t L = 1; L <= 8; L++) {
+      const uint32_t cL = (uint32_t)(T.cnt >> (8 * (L - 1))) & 0xFF;
+      const uint32_t cd = w8 >> (8 - L);
+      if (mL == 0 && cd < cL + first) {
+        mL = L;
+        neg = cd < first;
+        r = cd - first;
+      }
+      first = ((first + cL) << 1) & 0xFF;
+    }
+    if (mL == 0) {
+      code = (bp + 8 > T.nbits) ? 10 : 11;
+      break;
+    }
+    if (bp + mL > T.nbits || neg) {
+      code = 10;
+      break;
+    }
+    uint32_t i = 3, vbit = 0;
+    while (i - 3 < T.tb) {
+      const uint32_t info = c.byte(i);
+      const uint32_t n = (info & 31) + 1;
+      if ((info >> 5) + 1 == mL) {
+        if (r < n) {
+          vbit = 8 * (i + 1) + 11 * r;
           break;
         }
-        cnt += (uint64_t)n << (8 * (L - 1));
-        i += 1 + nbytes;
+        r -= n;
       }
-      if (!code) {
-        // offsets of each length's symbols in the flat table
-        uint64_t offs = 0;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int L = 0; L < 8; L++) {
-          offs |= (uint64_t)acc << (8 * L);
-          acc += (uint32_t)(cnt >> (8 * L)) & 0xFF;
-        }
-        // pass 2: unpack the 11-bit values (unpack11bit)
-        uint64_t run = 0;
-        i = 3;
-        while (i - 3 < tb) {
-          const uint32_t info = c[i++];
-          const uint32_t L = (info >> 5) + 1, n = (info & 31) + 1;
-          const uint32_t base = (uint32_t)(offs >> (8 * (L - 1))) & 0xFF;
-          const uint32_t done = (uint32_t)(run >> (8 * (L - 1))) & 0xFF;
-          for (uint32_t k = 0; k < n; k++) {
-            const uint32_t bit = 11 * k;
-            const uint32_t q = i + (bit >> 3);
-            const uint32_t raw = (uint32_t)c[q] | ((uint32_t)c[q + 1] << 8) | ((uint32_t)c[q + 2] << 16);
-            const uint32_t u = (raw >> (bit & 7)) & 0x7FF;
-            sym_at(base + done + k) = (uint16_t)(u >= 1024 ? u - 2048 : u);
-          }
-          run += (uint64_t)n << (8 * (L - 1));
-          i += (n * 11 + 7) / 8;
-        }
-        // symbols
-        const uint32_t bits = 3 + tb;
-        uint32_t bp = 0;
-        uint32_t j = 0;
-        while (bp < nbits && j < 64) {
-          const uint32_t q = bp >> 3;
-          const uint32_t x = (uint32_t)c[bits + q] | ((uint32_t)c[bits + q + 1] << 8);
-          const uint32_t w8 = __brev((x >> (bp & 7)) & 0xFF) >> 24;  // next 8 bits, MSB-first
-          uint32_t first = 0, mL = 0, mIdx = 0;
-          bool neg = false;
-#pragma unroll
-          for (uint32_t L = 1; L <= 8; L++) {
-            const uint32_t cL = (uint32_t)(cnt >> (8 * (L - 1))) & 0xFF;
-            const uint32_t cd = w8 >> (8 - L);
-            if (mL == 0 && cd < cL + first) {
-              mL = L;
-              neg = cd < first;
-              mIdx = ((uint32_t)(offs >> (8 * (L - 1))) & 0xFF) + (cd - first);
-            }
-            first = ((first + cL) << 1) & 0xFF;
-          }
-          if (mL == 0) {
-            code = (bp + 8 > nbits) ? 10 : 11;
-            break;
-          }
-          if (bp + mL > nbits || neg) {
-            code = 10;
-            break;
-          }
-          out_at(j++) = sym_at(mIdx);
-          bp += mL;
-        }
-      }
+      i += 1 + (n * 11 + 7) / 8;
     }
+    const uint32_t z = c_zz_dev[j];
+    out[coef_quad(g, z >> 3) * 8 + (z & 7)] = (uint16_t)(((int32_t)(c.bits32(vbit) << 21)) >> 21);
+    bp += mL;
+    j++;
+  }
+  for (; j < 64; j++) {
+    const uint32_t z = c_zz_dev[j];
+    out[coef_quad(g, z >> 3) * 8 + (z & 7)] = 0;
   }
   return code;
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void k_huff_decode(const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_t* __restrict__ in,
                                                    const uint32_t* __restrict__ in_size,
                                                    uint32_t cap,
                                                    const StreamDesc* __restrict__ desc,
@@ -166,9 +285,7 @@ __global__ __launch_bounds__(64) void k_huff_decode(const uint8_t* __restrict__ 
                                                    uint32_t tiles_p1,
                                                    uint4* __restrict__ coef,
                                                    unsigned long long* __restrict__ err) {
-  __shared__ uint32_t stage[kStageWords];
-  __shared__ uint32_t symw[32 * kWave];
-  __shared__ uint32_t outw[32 * kOutStride];
+  __shared__ uint4 stq[kStageQuads];
   if (desc->bad) return;
   const int lane = threadIdx.x;
   const uint32_t t = blockIdx.x;
@@ -179,13 +296,18 @@ __global__ __launch_bounds__(64) void k_huff_decode(const uint8_t* __restrict__ 
   const uint32_t g = g0 + lane;
   const bool live = g < g1;
   const uint32_t limit = min(*in_size, cap);
+  const uint32_t nblk = G.cum[3];
 
-  const uint32_t plane_pre = local_off[G.cum[p]] + tile_pre[G.cum[p] / kScanTile];
-  const uint32_t gl = live ? g : g1 - 1;
-  const uint32_t rel = local_off[gl] + tile_pre[gl / kScanTile] - plane_pre;
-  const uint32_t s = in[desc->sizes_pos[p] + (gl - G.cum[p])];
+  // end of the wave's chunk range from the scan alone (rel(nblk) = the total)
+  const uint32_t plane_pre = scanned(local_off, tile_pre, G.cum[p]);
+  const uint32_t end_scan = g1 == nblk ? tile_pre[(nblk + kScanTile - 1) / kScanTile]
+                                       : scanned(local_off, tile_pre, g1);
   const uint32_t cpos = desc->content_pos[p];
   const uint32_t csize = desc->content_size[p];
+  const uint32_t E = cpos + min(end_scan - plane_pre, csize);
+  const uint32_t gl = live ? g : g1 - 1;
+  const uint32_t rel = scanned(local_off, tile_pre, gl) - plane_pre;
+  const uint32_t s = in[desc->sizes_pos[p] + (gl - G.cum[p])];
 
   // plane-level check (DCT.cpp:21-33 reads past content_size otherwise):
   // the chunks must fit the declared content.
@@ -195,68 +317,85 @@ __global__ __launch_bounds__(64) void k_huff_decode(const uint8_t* __restrict__ 
     ok = false;
   }
 
-  // ---- stage [cpos + rel(g0), cpos + rel(g1-1) + s(g1-1)) into LDS
-  const uint32_t first_rel = __shfl(rel, 0, 64);
-  const uint32_t last_end = __shfl(rel + s, (int)(g1 - 1 - g0), 64);
-  const uint32_t a0 = cpos + first_rel;
-  const uint32_t a1 = min(cpos + min(last_end, csize), limit);
-  const uint32_t aw = a0 & ~3u;
-  const uint32_t nwords = a1 > aw ? (a1 - aw + 3) >> 2 : 0;
-  const bool fits = nwords + 2 <= (uint32_t)kStageWords;  // keep >= 8 B of zero slack
-  for (uint32_t i = lane; i < kStageWords; i += kWave) {
-    uint32_t v = 0;
-    if (i < nwords) {
-      const uint32_t a = aw + 4 * i;
-      if (a + 4 <= limit) {
-        v = *reinterpret_cast<const uint32_t*>(in + a);
-      } else {
-        for (uint32_t k = 0; k < 4; k++)
-          if (a + k < limit) v |= (uint32_t)in[a + k] << (8 * k);
-      }
-    }
-    stage[i] = v;
-  }
+  uint32_t nw[32];
 #pragma unroll
-  for (int w = 0; w < 32; w++) outw[w * kOutStride + lane] = 0;
-  __syncthreads();
-
-  const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage);
-  uint8_t* symb = reinterpret_cast<uint8_t*>(symw);
-  auto sym_at = [&](uint32_t i) -> uint16_t& {
-    return *reinterpret_cast<uint16_t*>(symb + (((i >> 1) * kWave + lane) * 4 + (i & 1) * 2));
-  };
-  uint8_t* outb = reinterpret_cast<uint8_t*>(outw);
-  auto out_at = [&](uint32_t j) -> uint16_t& {
-    return *reinterpret_cast<uint16_t*>(outb + (((j >> 1) * kOutStride + lane) * 4 + (j & 1) * 2));
-  };
-
+  for (int w = 0; w < 32; w++) nw[w] = 0;
   int code = 0;
-  if (ok) {
-    const uint32_t lb = a0 + rel - first_rel - aw;  // chunk start in the stage
-    if (fits) {
-      code = decode_chunk(LdsBytes{sb + lb}, s, sym_at, out_at);
-    } else {
-      const uint32_t abs0 = cpos + rel;
-      code = decode_chunk(GlobalBytes{in, abs0, limit}, s, sym_at, out_at);
-    }
-    if (code) record_error(err, 2ull * g + 1, code);
-  }
-  __syncthreads();
+  bool direct = false;  // block written by decode_general
 
-  // ---- write-out: zig-zag words from LDS, natural words to the quad layout
-  // (Huffman.cpp:148-153 de-zig-zag; 1 KiB contiguous per quad store)
-  if (live) {
-    uint32_t zw[32];
+  // Rounds: stage the chunks of the first pending lane onwards (as many as
+  // the stage holds, bytes at or past `limit` read as 0, one zero quad after),
+  // decode the lanes whose chunks are inside.  Chunks are consecutive and at
+  // most 255 B, so every round retires at least one lane; a 4K frame at q=50
+  // needs one round per wave.
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  uint64_t pending = __ballot(ok);
+  while (pending) {
+    const int lo = __ffsll((long long)pending) - 1;
+    const uint32_t A = cpos + __shfl(rel, lo, 64);
+    const uint32_t aw = A & ~15u;
+    const uint32_t wend = aw + 16 * (kStageQuads - 1);
+    const uint32_t nq = (min(E, wend) - aw + 15) >> 4;
+    const uint32_t nfull = limit >= aw ? min(nq, (limit - aw) >> 4) : 0;  // quads below limit
+    // the first 256 quads: loads at clamped addresses, all in flight before
+    // the first LDS write
+    uint4 r[4] = {zero, zero, zero, zero};
+    if (nfull > 0) {
 #pragma unroll
-    for (int w = 0; w < 32; w++) zw[w] = outw[w * kOutStride + lane];
-    uint32_t nw[32];
+      for (int m = 0; m < 4; m++) {
+        const uint32_t k = min(lane + 64u * m, nfull - 1);
+        r[m] = *reinterpret_cast<const uint4*>(in + aw + 16 * k);
+      }
 #pragma unroll
-    for (int m = 0; m < 32; m++) {
-      const int z0 = c_izz[2 * m], z1 = c_izz[2 * m + 1];
-      const uint32_t lo = (zw[z0 >> 1] >> (16 * (z0 & 1))) & 0xFFFFu;
-      const uint32_t hi = (zw[z1 >> 1] >> (16 * (z1 & 1))) & 0xFFFFu;
-      nw[m] = lo | (hi << 16);
+      for (int m = 0; m < 4; m++)
+        asm volatile("" : "+v"(r[m].x), "+v"(r[m].y), "+v"(r[m].z), "+v"(r[m].w));
     }
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const uint32_t k = lane + 64 * m;
+      if (k < nfull) stq[k] = r[m];
+    }
+    for (uint32_t k = lane + 256; k < nfull; k += 64)
+      stq[k] = *reinterpret_cast<const uint4*>(in + aw + 16 * k);
+    for (uint32_t k = nfull + lane; k <= nq; k += 64) {  // at or past `limit`, and the slack quad
+      uint32_t v[4] = {0, 0, 0, 0};
+      if (k < nq) {
+#pragma unroll
+        for (uint32_t b = 0; b < 16; b++) {
+          const uint32_t a = aw + 16 * k + b;
+          if (a < limit) v[b >> 2] |= (uint32_t)in[a] << (8 * (b & 3));
+        }
+      }
+      stq[k] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    __syncthreads();
+
+    const bool mine = ((pending >> lane) & 1) && cpos + rel + s <= wend;
+    const LdsChunk lc{reinterpret_cast<const uint32_t*>(stq), mine ? cpos + rel - aw : 0u};
+    Table T;
+    int pcode = 0;
+#if MYYUV_K5_EXP != 2
+    if (mine) pcode = parse_table(lc, s, T);
+#endif
+    const bool go = mine && pcode == 0;
+    int dcode;
+#if MYYUV_K5_EXP == 0
+    dcode = decode_regular(lc, T, go && T.regular, nw);
+#else
+    dcode = 0;
+#endif
+    if (go && !T.regular) {
+      direct = true;
+      dcode = decode_general(lc, T, coef, g);
+    }
+    if (mine) code = go ? dcode : pcode;
+    pending &= ~__ballot(mine);
+    __syncthreads();  // the next round overwrites the stage
+  }
+  if (ok && code) record_error(err, 2ull * g + 1, code);
+
+  // ---- natural-order words to the quad layout (1 KiB contiguous per store)
+  if (live && !direct) {
 #pragma unroll
     for (int c = 0; c < 8; c++)
       coef[coef_quad(g, c)] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);

@@ -634,6 +634,24 @@ int myyuv_debug_k2_stamps(unsigned long long out[40]) {
 #endif
 }
 
+// Diagnostic: the coefficient image of the last compress/decompress (natural
+// order, the quad layout of codec_common.hpp), n blocks, as int16[n][64].
+int myyuv_debug_coef(myyuv_hip_handle c, int16_t* out, uint32_t n) {
+  if (!c || !out) return MYYUV_E_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const size_t nq = (size_t)ceil_div(n, kWave) * kCoefQuadsPerWave;
+  if (nq * 16 > c->coef.n) return MYYUV_E_ARG;
+  std::vector<uint4> img(nq);
+  if (hipStreamSynchronize(c->stream) != hipSuccess ||
+      hipMemcpy(img.data(), c->coef.p, nq * 16, hipMemcpyDeviceToHost) != hipSuccess)
+    return MYYUV_E_HIP;
+  for (uint32_t b = 0; b < n; b++)
+    for (uint32_t q = 0; q < 8; q++)
+      std::memcpy(out + (size_t)b * 64 + q * 8, &img[coef_quad(b, q)], 16);
+  return 0;
+}
+
 // ---- block-level KAT entry points -----------------------------------------
 int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblocks,
                           const float qtable[64], int16_t* coef_zz) {
