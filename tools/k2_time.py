@@ -15,7 +15,7 @@ from oracle import oracle as O  # noqa: E402
 
 c = myyuv_hip.Codec(0)
 L = myyuv_hip.load()
-names = ['', 'symbols', 'map', 'heap+len', 'sort', 'emit']
+names = ['', 'symbols', 'map', 'heap+len', 'canon', 'emit']
 
 
 def run(raw, w, h, q, label, iters=10):
@@ -36,13 +36,19 @@ def run(raw, w, h, q, label, iters=10):
     L.myyuv_debug_k2_stamps(st)
     ks = c.kernel_stats()
     c.profile(False)
-    nw = ((w * h * 3 // 2) // 64 + 63) // 64 * iters
-    fast = {names[k]: round(st[k] / nw) for k in range(1, 6)}
+    import numpy as np
+    fs = np.zeros(8192 * 8, np.uint32)
+    L.myyuv_debug_k2_fstamps(fs.ctypes.data_as(ctypes.c_void_p), 8192)
+    fs = fs.reshape(-1, 8)[:, 1:6]
+    fs = fs[fs.sum(1) > 0]
+    fast = {names[k + 1]: int(fs[:, k].mean()) for k in range(5)}
+    fast_max = {names[k + 1]: int(fs[:, k].max()) for k in range(5)}
     wide_sum = {names[k]: st[k + 8] for k in range(1, 6)}
     wide_max = {names[k]: st[k + 16] for k in range(1, 6)}
     us = lambda k: round(ks[k][0] / max(ks[k][1], 1) * 1e3, 1)
     print(f"{label}: fast {us('huff_encode')} us, wide {us('huff_encode_wide')} us", flush=True)
-    print("   fast cycles/wave", fast, flush=True)
+    print("   fast cycles/wave mean", fast, flush=True)
+    print("   fast cycles/wave max", fast_max, "total mean", int(fs.sum(1).mean()), "max", int(fs.sum(1).max()), flush=True)
     print("   wide cycles summed", wide_sum, flush=True)
     print("   wide cycles max/wave", wide_max, flush=True)
     wn = ['', 'load', 'distinct', 'map', 'heap', 'len', 'canon', 'emit']

@@ -89,6 +89,10 @@ constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
 // (k_huff_encode_wave), longer ones lane-per-block (k_huff_encode_wide).
 constexpr uint32_t kWaveEncodeLimit = 24576;
 constexpr uint32_t kWaveEncodeGrid = 16384;  // waves of k_huff_encode_wave
+#ifndef MYYUV_K2_GROUP
+#define MYYUV_K2_GROUP 256
+#endif
+constexpr uint32_t kK2Group = MYYUV_K2_GROUP;  // blocks per workgroup of k_huff_encode
 __host__ __device__ __forceinline__ uint32_t coef_quad(uint32_t g, uint32_t c) {
   return ((g >> 6) * 8u + c) * 64u + (g & 63u);
 }

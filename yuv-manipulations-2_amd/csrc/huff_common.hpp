@@ -1,0 +1,522 @@
+// huff_common.hpp — pieces of K2 (Huffman::fromData + Huffman::dump,
+// myyuv_DCT/Huffman.cpp:172-241, :279-326) shared by the kernels in
+// k_huff_encode.hip and compiled for the host as well (MYYUV_HD), so the
+// register-resident encoder's logic can be checked against the oracle on the
+// CPU (tools/r8_host.cpp, tests/test_r8_host.py).  The device build is the
+// product; the host build is test infrastructure.
+#pragma once
+#include "codec_common.hpp"
+
+#define MYYUV_HD __host__ __device__ __forceinline__
+
+// diagnostic hook (k_huff_encode.hip's stamp build): per-phase wave cycles
+#ifndef R8_STAMP
+#define R8_STAMP(k) \
+  do {              \
+  } while (0)
+#define R8_STAMP_DECL
+#endif
+
+namespace myyuv_gpu {
+
+MYYUV_HD uint32_t hd_umulhi(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+}
+MYYUV_HD uint32_t hd_brev(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __brev(x);
+#else
+  uint32_t r = 0;
+  for (int i = 0; i < 32; i++) r |= ((x >> i) & 1u) << (31 - i);
+  return r;
+#endif
+}
+MYYUV_HD uint32_t hd_clz(uint32_t x) { return (uint32_t)__builtin_clz(x); }  // x != 0
+
+// Bucket-count phases of the prime rehash policy for <= 65 elements
+// (_Prime_rehash_policy::_M_next_bkt / _M_need_rehash): 13 buckets from the
+// first insert, 29 at the 14th, 59 at the 30th, 127 at the 60th element.
+struct Phase {
+  uint32_t nb, r64, magic;  // buckets, 2^64 mod nb, ceil(2^32 / nb)
+};
+MYYUV_HD constexpr uint32_t pow2_64_mod(uint32_t m) {
+  uint64_t r = 1;
+  for (int i = 0; i < 64; i++) r = (r * 2) % m;
+  return (uint32_t)r;
+}
+MYYUV_HD Phase phase_of(int ph) {
+  Phase p;
+  p.nb = ph == 0 ? 13u : ph == 1 ? 29u : ph == 2 ? 59u : 127u;
+  p.r64 = ph == 0   ? pow2_64_mod(13)
+          : ph == 1 ? pow2_64_mod(29)
+          : ph == 2 ? pow2_64_mod(59)
+                    : pow2_64_mod(127);
+  p.magic = ph == 0 ? 330382100u : ph == 1 ? 148102321u : ph == 2 ? 72796056u : 33818641u;
+  return p;
+}
+// hash(int16 v) % nb with hash = (size_t)(int64)v: v >= 0 -> v % nb,
+// v < 0 -> (2^64 + v) % nb = (r64 + v) % nb.  t < 2^17: the magic multiply
+// is exact.
+MYYUV_HD uint32_t bucket_of(int v, const Phase& P) {
+  const uint32_t t = (uint32_t)(v + (v < 0 ? (int)(P.r64 + 1024u * P.nb) : 0));
+  const uint32_t q = hd_umulhi(t, P.magic);
+  return t - q * P.nb;
+}
+
+// LSB-first bit writer into the block's output slot.
+struct BitWriter {
+  uint32_t* out;  // &slot word 0 of this block; words kWave apart
+  uint64_t acc = 0;
+  int nacc = 0;
+  int widx = 0;
+  MYYUV_HD void put(uint32_t v, int n) {
+    acc |= (uint64_t)v << nacc;
+    nacc += n;
+    if (nacc >= 32) {
+      out[widx * kWave] = (uint32_t)acc;
+      widx++;
+      acc >>= 32;
+      nacc -= 32;
+    }
+  }
+  MYYUV_HD void align_byte() { nacc = (nacc + 7) & ~7; }
+  MYYUV_HD void flush() {
+    if (nacc > 0) out[widx * kWave] = (uint32_t)acc;
+  }
+};
+
+// Per-position KC slot of the position's symbol, recorded while the distinct
+// symbols are found so the emitter indexes the code table directly instead of
+// probing the hash table again: kBits bits per position, positions static.
+template <int CAP>
+struct SlotIds {
+  static constexpr int kBits = CAP <= 8 ? 3 : (CAP <= 16 ? 4 : 6);
+  static constexpr int kPer = 32 / kBits;
+  static constexpr int kRegs = (64 + kPer - 1) / kPer;
+  uint32_t r[kRegs];
+  MYYUV_HD void clear() {
+#pragma unroll
+    for (int i = 0; i < kRegs; i++) r[i] = 0;
+  }
+  MYYUV_HD void set(int pos, uint32_t slot) {
+    r[pos / kPer] |= slot << (kBits * (pos % kPer));
+  }
+  MYYUV_HD uint32_t get(int pos) const {
+    return (r[pos / kPer] >> (kBits * (pos % kPer))) & ((1u << kBits) - 1u);
+  }
+};
+
+// The lane's block's coefficients (natural order, word w = coefficients 2w,
+// 2w+1), loaded once into registers: every loop over positions below is
+// unrolled, so sym(i) — the i-th coefficient in zig-zag order — is a static
+// register index and half.
+constexpr uint8_t c_zz[64] = MYYUV_ZIGZAG;
+
+struct CoefRegs {
+  uint32_t w[32];
+  __device__ __forceinline__ void load(const uint4* __restrict__ coef, uint32_t g) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint4 v = coef[coef_quad(g, c)];
+      w[4 * c] = v.x;
+      w[4 * c + 1] = v.y;
+      w[4 * c + 2] = v.z;
+      w[4 * c + 3] = v.w;
+    }
+  }
+  MYYUV_HD int sym(int i) const {
+    const int n = c_zz[i];
+    return (int)(int16_t)(w[n >> 1] >> (16 * (n & 1)));
+  }
+  // 1 + zig-zag index of the last nonzero coefficient (0: all zero)
+  MYYUV_HD int msz() const {
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      if (sym(i) != 0) m = i + 1;
+    return m;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Register-resident encoder for blocks with at most CAP (4 or 8) distinct
+// symbols, lane per block.  The LDS version of encode_block is a
+// chain of dependent LDS round trips per lane (probing, list and heap
+// surgery), so the longest lane of each wave sets the kernel time; here every
+// structure lives in registers and every dynamic index is a small select
+// network or a shift into a packed word:
+//   * keys: 12-bit tagged fields (0x800 | v & 0x7FF; 0 = empty), two per
+//     dword; one position is matched against all 8 keys with three SWAR ops
+//     per dword pair;
+//   * counts: 8 x u8 in a 64-bit word; per-position slot ids (3 bits);
+//   * unordered_map order in closed form (13 buckets: no rehash below 13
+//     symbols, so the freq[0] probe is invisible): runs of a bucket in
+//     decreasing first insertion, each run in decreasing insertion order;
+//   * the libstdc++ heap (push_heap / pop_heap, __adjust_heap) on 8 registers,
+//     specialised for at most 8 entries: pop's hole descends at most two
+//     levels and every child it compares is one of two candidates;
+//   * parents, depths, per-length counts, canonical first codes: packed
+//     nibble / byte fields.
+// Same bytes as encode_block.
+// ---------------------------------------------------------------------------
+
+namespace rr {
+
+MYYUV_HD uint32_t fq(uint32_t e) { return e >> 8; }
+
+// H[i] for a dynamic i in [0, CAP)
+template <int CAP>
+MYYUV_HD uint32_t hget(const uint32_t (&H)[CAP], uint32_t i) {
+  const uint32_t a = (i & 1) ? H[1] : H[0], b = (i & 1) ? H[3] : H[2];
+  const uint32_t ab = (i & 2) ? b : a;
+  if constexpr (CAP == 4) {
+    return ab;
+  } else {
+    const uint32_t c = (i & 1) ? H[5] : H[4], d = (i & 1) ? H[7] : H[6];
+    const uint32_t cd = (i & 2) ? d : c;
+    return (i & 4) ? cd : ab;
+  }
+}
+// H[i] = x for a dynamic i in [lo, hi]
+template <int lo, int hi, int CAP>
+MYYUV_HD void hset(uint32_t (&H)[CAP], uint32_t i, uint32_t x) {
+#pragma unroll
+  for (int s = lo; s <= hi; s++) H[s] = i == (uint32_t)s ? x : H[s];
+}
+
+// __push_heap from `hole` (in [0, maxhole]): sift up while parent.freq > e.freq.
+template <int maxhole, int CAP>
+MYYUV_HD void sift_up(uint32_t (&H)[CAP], uint32_t hole, uint32_t e) {
+  bool go = true;
+#pragma unroll
+  for (int lvl = 0; lvl < 3; lvl++) {
+    if ((maxhole >> lvl) == 0) break;  // hole < 2^(lvl): nothing above
+    const uint32_t par = (hole - 1) >> 1;
+    const uint32_t pe = hget<CAP>(H, par);
+    const bool mv = go && hole > 0 && fq(pe) > fq(e);
+    // hole's possible values at this level: [1, maxhole >> lvl] roughly; the
+    // select network covers [1, 7] and folds for static holes
+    if (mv) hset<1, CAP - 1>(H, hole, pe);
+    hole = mv ? par : hole;
+    go = mv;
+  }
+  hset<0, CAP - 1>(H, hole, e);
+}
+
+// std::priority_queue::pop (libstdc++ __pop_heap + __adjust_heap) for a heap
+// of len in [1, CAP] entries; returns the old top.
+template <int CAP>
+MYYUV_HD uint32_t pop(uint32_t (&H)[CAP], uint32_t& len) {
+  const uint32_t top = H[0];
+  const uint32_t m = --len;  // entries left
+  if (m > 0) {
+    const uint32_t value = hget<CAP>(H, m);
+    // __adjust_heap(first, 0, m, value): second child walk
+    uint32_t hole = 0, sc = 0;
+    const bool it1 = m >= 3;  // 0 < (m - 1) / 2
+    const uint32_t c1 = fq(H[2]) > fq(H[1]) ? 1u : 2u;
+    if (it1) {
+      H[0] = c1 == 1 ? H[1] : H[2];
+      hole = c1;
+      sc = c1;
+    }
+    if constexpr (CAP == 8) {
+      const bool it2 = it1 && (c1 == 1 ? m >= 5 : m >= 7);  // sc < (m - 1) / 2
+      const uint32_t rt = c1 == 1 ? H[4] : H[6], lt = c1 == 1 ? H[3] : H[5];
+      const bool left = fq(rt) > fq(lt);
+      const uint32_t c2 = 2 * c1 + 2 - (left ? 1u : 0u);
+      if (it2) {
+        const uint32_t pv = left ? lt : rt;
+        H[1] = c1 == 1 ? pv : H[1];
+        H[2] = c1 == 2 ? pv : H[2];
+        hole = c2;
+        sc = c2;
+      }
+    }
+    // even length, last internal node with a single child
+    if ((m & 1) == 0 && sc == (m - 2) / 2) {
+      const uint32_t ch = 2 * sc + 1;  // (m, sc) in {(2,0), (4,1), (6,2)}
+      if constexpr (CAP == 4) {
+        H[0] = H[1];  // m = 2
+      } else {
+        const uint32_t cv = sc == 0 ? H[1] : (sc == 1 ? H[3] : H[5]);
+        H[0] = sc == 0 ? cv : H[0];
+        H[1] = sc == 1 ? cv : H[1];
+        H[2] = sc == 2 ? cv : H[2];
+      }
+      hole = ch;
+    }
+    sift_up<CAP - 2, CAP>(H, hole, value);
+  }
+  return top;
+}
+
+// field i (dynamic, [0, CAP)) of CAP x 16-bit fields in CAP / 2 dwords
+// (the dwords are copied to scalars first: a select between two elements of
+// a local array gets folded into one dynamically indexed load, which sends
+// the whole array to scratch)
+template <int CAP>
+MYYUV_HD uint32_t f16(const uint32_t (&a)[CAP / 2], uint32_t i) {
+  const uint32_t a0 = a[0], a1 = a[1];
+  uint32_t d = (i & 2) ? a1 : a0;
+  if constexpr (CAP == 8) {
+    const uint32_t a2 = a[2], a3 = a[3];
+    d = (i & 4) ? ((i & 2) ? a3 : a2) : d;
+  }
+  return d >> ((i & 1) * 16) & 0xFFFFu;
+}
+
+}  // namespace rr
+
+template <int CAP>
+MYYUV_HD bool encode_block_r(const CoefRegs& R, int msz, int wave_msz,
+                                                uint32_t* __restrict__ slot,
+                                                uint8_t* __restrict__ size_out) {
+  using namespace rr;
+  static_assert(CAP == 4 || CAP == 8, "CAP");
+  constexpr int NP = CAP / 2;
+  R8_STAMP_DECL
+  R8_STAMP(0);
+  // ---------------- 1. distinct symbols, counts, per-position slots ----------------
+  uint32_t KP[NP] = {};  // tagged keys, field k = slot k
+  uint64_t cnt = 0;               // count of slot k in byte k
+  uint32_t n = 0;
+  bool has_zero = false, ovf = false;
+  SlotIds<CAP> ids;
+  ids.clear();
+#pragma unroll
+  for (int i0 = 0; i0 < 64; i0 += 8) {
+    if (i0 < wave_msz) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = i0 + k;
+        const int v = R.sym(i);
+        const bool act = i < msz && !ovf;
+        const uint32_t f = 0x800u | ((uint32_t)v & 0x7FFu);
+        const uint32_t vv = f | (f << 16);
+        uint32_t oh = 0;  // one-hot over slots: pair p's fields at bits 15 - p / 31 - p
+#pragma unroll
+        for (int p = 0; p < NP; p++)
+          oh |= (~(((KP[p] ^ vv) | 0x80008000u) - 0x00010001u) & 0x80008000u) >> p;
+        const bool found = oh != 0;
+        const uint32_t b = 31u - hd_clz(oh | 1u);  // the one set bit: 12..15 or 28..31 when found
+        const uint32_t idx = b >= 28 ? 2 * (31 - b) + 1 : 2 * (15 - b);
+        const bool add = act && !found;
+        ovf = ovf || (add && n == CAP);
+        const bool ins = add && n < CAP;
+        const uint32_t sl = found ? idx : n;
+        const uint32_t ishift = (n & 1) * 16;
+#pragma unroll
+        for (int p = 0; p < NP; p++) KP[p] |= (ins && (n >> 1) == (uint32_t)p) ? f << ishift : 0u;
+        if (act) cnt += 1ull << (8 * (sl & 7));
+        n += ins ? 1u : 0u;
+        has_zero = has_zero || (act && v == 0);
+        ids.set(i, act ? (sl & 7) : 0u);
+      }
+    }
+  }
+  if (ovf) return false;
+  if (msz == 0) {  // all-zero block: one symbol 0, count 1 (Huffman.cpp:191-194)
+    KP[0] = 0x800u;
+    cnt = 1;
+    n = 1;
+    msz = 1;
+    has_zero = true;
+  }
+
+  R8_STAMP(1);
+  // ---------------- 2. unordered_map iteration order (13 buckets) ----------------
+  int key[CAP];
+  uint32_t bk[CAP];
+  const Phase P0 = phase_of(0);
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    key[k] = (int)((KP[k >> 1] >> (16 * (k & 1))) << 21) >> 21;
+    bk[k] = bucket_of(key[k], P0);
+  }
+  uint32_t F[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    uint32_t f = (uint32_t)k;
+#pragma unroll
+    for (int j = k - 1; j >= 0; j--) f = bk[j] == bk[k] ? (uint32_t)j : f;
+    F[k] = f;
+  }
+  uint32_t ord = 0;  // walk position r -> slot, nibble r
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    uint32_t rank = 0;
+#pragma unroll
+    for (int j = 0; j < CAP; j++) {
+      if (j == k) continue;
+      const bool before = F[j] > F[k] || (F[j] == F[k] && j > k);
+      rank += ((uint32_t)j < n && before) ? 1u : 0u;
+    }
+    if ((uint32_t)k < n) ord |= (uint32_t)k << (4 * rank);
+  }
+
+  R8_STAMP(2);
+  // ---------------- 3. Huffman merges on the libstdc++ heap ----------------
+  uint32_t H[CAP] = {};
+  uint32_t hlen = 0;
+#pragma unroll
+  for (int r = 0; r < CAP; r++) {
+    if ((uint32_t)r < n) {
+      const uint32_t k = (ord >> (4 * r)) & 15u;
+      const uint32_t e = (((uint32_t)(cnt >> (8 * k)) & 0xFFu) << 8) | k;
+      sift_up<CAP - 1, CAP>(H, (uint32_t)r, e);
+      hlen++;
+    }
+  }
+  uint32_t lpar = 0, ipar = 0;  // parent (merge index) of leaf k / internal j, nibbles
+#pragma unroll
+  for (int j = 0; j < CAP - 1; j++) {
+    if ((uint32_t)j + 1 < n) {
+      const uint32_t l = pop<CAP>(H, hlen);
+      const uint32_t r = pop<CAP>(H, hlen);
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        const uint32_t id = (s == 0 ? l : r) & 0xFFu;
+        const uint32_t sh = 4 * (id & 7u);
+        const uint32_t m = ~(15u << sh), v = (uint32_t)j << sh;
+        if (id < 8) lpar = (lpar & m) | v;
+        else ipar = (ipar & m) | v;
+      }
+      sift_up<CAP - 2, CAP>(H, hlen, ((fq(l) + fq(r)) << 8) | (8u + (uint32_t)j));
+      hlen++;
+    }
+  }
+  // depths of internal nodes (root = n - 2 at depth 0), then code lengths
+  uint32_t dep = 0;
+#pragma unroll
+  for (int j = CAP - 3; j >= 0; j--) {
+    if ((uint32_t)j + 2 < n) {
+      const uint32_t par = (ipar >> (4 * j)) & 15u;
+      dep |= (((dep >> (4 * par)) & 15u) + 1u) << (4 * j);
+    }
+  }
+  uint32_t len[CAP];
+  uint32_t nbits = 0;
+  uint64_t lcount = 0;  // 8 x u8 per-length counts
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    const uint32_t par = (lpar >> (4 * k)) & 15u;
+    len[k] = n >= 2 ? ((dep >> (4 * par)) & 15u) + 1u : 1u;
+    if ((uint32_t)k < n) {
+      nbits += ((uint32_t)(cnt >> (8 * k)) & 0xFFu) * len[k];
+      lcount += 1ull << (8 * (len[k] - 1));
+    }
+  }
+
+  R8_STAMP(3);
+  // ---------------- 4. canonical order (length, symbol) and codes ----------------
+  uint32_t crank[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    const uint32_t ck = (len[k] << 11) | (uint32_t)(key[k] + 1024);
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < CAP; j++) {
+      if (j == k) continue;
+      const uint32_t cj = (len[j] << 11) | (uint32_t)(key[j] + 1024);
+      r += ((uint32_t)j < n && cj < ck) ? 1u : 0u;
+    }
+    crank[k] = (uint32_t)k < n ? r : 0xFFu;  // unused slots rank nowhere
+  }
+  uint64_t fc64 = 0;  // per length: first code
+  uint32_t fr32 = 0;            // per length: first canonical rank
+  uint32_t table_bytes = 0;
+  {
+    uint32_t fc = 0, fr = 0;
+#pragma unroll
+    for (int l = 0; l < 8; l++) {
+      const uint32_t c = (uint32_t)(lcount >> (8 * l)) & 0xFFu;
+      fc64 |= (uint64_t)(fc & 0xFFu) << (8 * l);
+      fr32 |= fr << (4 * l);
+      table_bytes += c ? 1 + (c * 11 + 7) / 8 : 0;  // c <= CAP: one group per length
+      fc = (fc + c) << 1;
+      fr += c;
+    }
+  }
+  uint32_t CT[NP] = {};  // per slot: len << 8 | reversed code
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    const uint32_t L = len[k] - 1;
+    const uint32_t code = (uint32_t)(fc64 >> (8 * L)) + crank[k] - ((fr32 >> (4 * L)) & 15u);
+    const uint32_t rcode = hd_brev(code) >> (32 - len[k]);
+    CT[k >> 1] |= ((len[k] << 8) | (rcode & 0xFFu)) << (16 * (k & 1));
+  }
+
+  R8_STAMP(4);
+  // ---------------- 5. chunk bytes (Huffman.cpp:279-326) ----------------
+  BitWriter bw;
+  bw.out = slot;
+  bw.put(nbits, 16);
+  bw.put(table_bytes, 8);
+  // table: canonical order; a group header where the length changes
+  uint32_t curlen = 0;
+#pragma unroll
+  for (int r = 0; r < CAP; r++) {
+    if ((uint32_t)r < n) {
+      uint32_t kl = 0;  // key & 0x7FF | len << 11 of the symbol ranked r
+#pragma unroll
+      for (int k = 0; k < CAP; k++)
+        kl = crank[k] == (uint32_t)r ? (((uint32_t)key[k] & 0x7FFu) | (len[k] << 11)) : kl;
+      const uint32_t L = kl >> 11;
+      if (L != curlen) {
+        bw.align_byte();
+        const uint32_t c = (uint32_t)(lcount >> (8 * (L - 1))) & 0xFFu;
+        bw.put(((L - 1) << 5) | (c - 1), 8);
+        curlen = L;
+      }
+      bw.put(kl & 0x7FFu, 11);  // pack11bit
+    }
+  }
+  bw.align_byte();
+#pragma unroll
+  for (int i0 = 0; i0 < 64; i0 += 8) {
+    if (i0 < wave_msz) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = i0 + k;
+        if (i < msz) {
+          const uint32_t ct = f16<CAP>(CT, ids.get(i));
+          bw.put(ct & 0xFFu, (int)(ct >> 8));
+        }
+      }
+    }
+  }
+  bw.flush();
+  *size_out = (uint8_t)(3 + table_bytes + (nbits + 7) / 8);
+  R8_STAMP(5);
+  return true;
+}
+
+// K2 block classes (k_huff_encode sorts a workgroup's blocks by class so each
+// wave runs the cheapest encoder that fits all its blocks):
+//   single: msz <= 1, one symbol;  r4 / r8: at most 4 / 8 distinct symbols
+//   for sure (nonzero coefficients, plus one for a zero inside the message);
+//   r8x: the rest, encode_block_r<8> with the overflow worklist behind it.
+constexpr uint32_t kClassSingle = 0, kClassR4 = 1, kClassR8 = 2, kClassR8x = 3, kClassDead = 4;
+MYYUV_HD uint32_t block_class(const CoefRegs& R, int msz) {
+  if (msz <= 1) return kClassSingle;
+  uint32_t nnz = 0;
+#pragma unroll
+  for (int w = 0; w < 32; w++) nnz += ((R.w[w] & 0xFFFFu) != 0) + ((R.w[w] >> 16) != 0);
+  const uint32_t nub = nnz + ((uint32_t)msz > nnz ? 1u : 0u);
+  return nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
+}
+
+// Blocks whose message is one symbol (msz <= 1: all zero, or the DC
+// coefficient alone; Huffman.cpp:191-194 for the all-zero case): one code of
+// length 1, one table group; the chunk is 7 bytes:
+//   u16 nbits = 1, u8 table_bytes = 3, group header 0x00, 11-bit key, 1 code byte 0.
+MYYUV_HD void encode_block_single(const CoefRegs& R, uint32_t* __restrict__ slot,
+                                  uint8_t* __restrict__ size_out) {
+  const uint32_t key = (uint32_t)R.sym(0) & 0x7FFu;
+  slot[0] = 1u | (3u << 16);
+  slot[kWave] = key;
+  *size_out = 7;
+}
+
+}  // namespace myyuv_gpu

@@ -44,6 +44,22 @@
 //            heap (u16 freq<<8 | id; internal node k keeps depth<<8 | parent in
 //            slot CAP-1-k), then the canonical order (u8).
 #include "codec_common.hpp"
+#ifdef MYYUV_STAMPS
+namespace myyuv_gpu {
+extern __device__ uint32_t g_k2_fstamps[8192 * 8];
+}
+#define R8_STAMP_DECL unsigned long long _r8prev = 0;
+#define R8_STAMP(k)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();                             \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    if ((threadIdx.x & 63) == 0 && (k) > 0 && blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6) < 8192) \
+      g_k2_fstamps[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = (uint32_t)(_t - _r8prev); \
+    _r8prev = _t;                                                                     \
+  } while (0)
+#endif
+#include "huff_common.hpp"
 
 namespace myyuv_gpu {
 
@@ -51,14 +67,21 @@ namespace myyuv_gpu {
 // diagnostic build only: per-stage wave cycles — [0..7] fast pass summed
 // over waves, [8..15] wide pass summed, [16..23] wide pass max over waves
 __device__ unsigned long long g_k2_stamps[40];
+// per-wave stage cycles of the CAP=8 pass (plain stores: contended atomics
+// would distort the timing): g_k2_fstamps[wave][8]
+__device__ uint32_t g_k2_fstamps[8192 * 8];
 #define STAMP(k)                                                                     \
   do {                                                                               \
     __builtin_amdgcn_sched_barrier(0);                                               \
     unsigned long long _t = __builtin_amdgcn_s_memtime();                            \
     __builtin_amdgcn_sched_barrier(0);                                               \
     if (threadIdx.x == 0 && (k) > 0) {                                               \
-      atomicAdd(&g_k2_stamps[(k) + (CAP > 8 ? 8 : 0)], _t - _tprev);                 \
-      if (CAP > 8) atomicMax(&g_k2_stamps[(k) + 16], _t - _tprev);                   \
+      if (CAP == 8) {                                                                \
+        if (blockIdx.x < 8192) g_k2_fstamps[blockIdx.x * 8 + (k)] = (uint32_t)(_t - _tprev); \
+      } else {                                                                       \
+        atomicAdd(&g_k2_stamps[(k) + 8], _t - _tprev);                               \
+        atomicMax(&g_k2_stamps[(k) + 16], _t - _tprev);                              \
+      }                                                                              \
     }                                                                                \
     _tprev = _t;                                                                     \
   } while (0)
@@ -126,36 +149,6 @@ __device__ __forceinline__ uint32_t nnext(uint32_t w) { return (w >> 18) & 127u;
 __device__ __forceinline__ uint32_t nbkt(uint32_t w) { return w >> 25; }
 __device__ __forceinline__ uint32_t set_next(uint32_t w, uint32_t nx) {
   return (w & ~(127u << 18)) | (nx << 18);
-}
-
-// Bucket-count phases of the prime rehash policy for <= 65 elements
-// (_Prime_rehash_policy::_M_next_bkt / _M_need_rehash): 13 buckets from the
-// first insert, 29 at the 14th, 59 at the 30th, 127 at the 60th element.
-struct Phase {
-  uint32_t nb, r64, magic;  // buckets, 2^64 mod nb, ceil(2^32 / nb)
-};
-__host__ __device__ constexpr uint32_t pow2_64_mod(uint32_t m) {
-  uint64_t r = 1;
-  for (int i = 0; i < 64; i++) r = (r * 2) % m;
-  return (uint32_t)r;
-}
-__device__ __forceinline__ Phase phase_of(int ph) {
-  Phase p;
-  p.nb = ph == 0 ? 13u : ph == 1 ? 29u : ph == 2 ? 59u : 127u;
-  p.r64 = ph == 0   ? pow2_64_mod(13)
-          : ph == 1 ? pow2_64_mod(29)
-          : ph == 2 ? pow2_64_mod(59)
-                    : pow2_64_mod(127);
-  p.magic = ph == 0 ? 330382100u : ph == 1 ? 148102321u : ph == 2 ? 72796056u : 33818641u;
-  return p;
-}
-// hash(int16 v) % nb with hash = (size_t)(int64)v: v >= 0 -> v % nb,
-// v < 0 -> (2^64 + v) % nb = (r64 + v) % nb.  t < 2^17: the magic multiply
-// is exact.
-__device__ __forceinline__ uint32_t bucket_of(int v, const Phase& P) {
-  const uint32_t t = (uint32_t)(v + (v < 0 ? (int)(P.r64 + 1024u * P.nb) : 0));
-  const uint32_t q = __umulhi(t, P.magic);
-  return t - q * P.nb;
 }
 
 // Slot lookup in the open-addressing table (any hash works here: it only
@@ -267,81 +260,6 @@ __device__ __forceinline__ uint32_t heap_pop(const Img<CAP>& I, int& len) {
   }
   return top;
 }
-
-// LSB-first bit writer into the block's output slot.
-struct BitWriter {
-  uint32_t* out;  // &slot word 0 of this block; words kWave apart
-  uint64_t acc = 0;
-  int nacc = 0;
-  int widx = 0;
-  __device__ __forceinline__ void put(uint32_t v, int n) {
-    acc |= (uint64_t)v << nacc;
-    nacc += n;
-    if (nacc >= 32) {
-      out[widx * kWave] = (uint32_t)acc;
-      widx++;
-      acc >>= 32;
-      nacc -= 32;
-    }
-  }
-  __device__ __forceinline__ void align_byte() { nacc = (nacc + 7) & ~7; }
-  __device__ __forceinline__ void flush() {
-    if (nacc > 0) out[widx * kWave] = (uint32_t)acc;
-  }
-};
-
-// Per-position KC slot of the position's symbol, recorded while the distinct
-// symbols are found so the emitter indexes the code table directly instead of
-// probing the hash table again: kBits bits per position, positions static.
-template <int CAP>
-struct SlotIds {
-  static constexpr int kBits = CAP <= 8 ? 3 : (CAP <= 16 ? 4 : 6);
-  static constexpr int kPer = 32 / kBits;
-  static constexpr int kRegs = (64 + kPer - 1) / kPer;
-  uint32_t r[kRegs];
-  __device__ __forceinline__ void clear() {
-#pragma unroll
-    for (int i = 0; i < kRegs; i++) r[i] = 0;
-  }
-  __device__ __forceinline__ void set(int pos, uint32_t slot) {
-    r[pos / kPer] |= slot << (kBits * (pos % kPer));
-  }
-  __device__ __forceinline__ uint32_t get(int pos) const {
-    return (r[pos / kPer] >> (kBits * (pos % kPer))) & ((1u << kBits) - 1u);
-  }
-};
-
-// The lane's block's coefficients (natural order, word w = coefficients 2w,
-// 2w+1), loaded once into registers: every loop over positions below is
-// unrolled, so sym(i) — the i-th coefficient in zig-zag order — is a static
-// register index and half.
-constexpr uint8_t c_zz[64] = MYYUV_ZIGZAG;
-
-struct CoefRegs {
-  uint32_t w[32];
-  __device__ __forceinline__ void load(const uint4* __restrict__ coef, uint32_t g) {
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const uint4 v = coef[coef_quad(g, c)];
-      w[4 * c] = v.x;
-      w[4 * c + 1] = v.y;
-      w[4 * c + 2] = v.z;
-      w[4 * c + 3] = v.w;
-    }
-  }
-  __device__ __forceinline__ int sym(int i) const {
-    const int n = c_zz[i];
-    return (int)(int16_t)(w[n >> 1] >> (16 * (n & 1)));
-  }
-  // 1 + zig-zag index of the last nonzero coefficient (0: all zero)
-  __device__ __forceinline__ int msz() const {
-    int m = 0;
-#pragma unroll
-    for (int i = 0; i < 64; i++)
-      if (sym(i) != 0) m = i + 1;
-    return m;
-  }
-};
 
 // The whole per-block program.  Returns false (and writes nothing) when the
 // block has more than CAP distinct symbols.
@@ -810,36 +728,99 @@ __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) encode_block_wave(coef, work[i], img, slots, sizes, i);
 }
 
-// Fast pass over every block (CAP=8); blocks with more distinct symbols are
-// appended to `work` for k_huff_encode_wide.
+// Fast pass over every block.  A workgroup takes kK2Group consecutive blocks,
+// classifies them (block_class: one symbol / <= 4 / <= 8 distinct for sure /
+// the rest), sorts them by class through LDS and hands each wave 64 blocks of
+// (nearly) one class, so a wave runs the cheapest register-resident encoder
+// that fits all its blocks and its loops run to the maxima of similar blocks
+// rather than of a 64-block stretch of the frame.  Sorted chunks are dealt to
+// the waves so that each SIMD gets one heavy and one light chunk.  Blocks with
+// more than 8 distinct symbols are appended to `work` for the overflow passes.
 //   coef: natural-order quads (codec_common.hpp);
 //   slots: [ceil(n/64)][40][64] u32; sizes: [n] u8.
-__global__ __launch_bounds__(64) void k_huff_encode(const uint4* __restrict__ coef,
-                                                   uint32_t nblocks,
-                                                   uint32_t* __restrict__ slots,
-                                                   uint8_t* __restrict__ sizes,
-                                                   uint32_t* __restrict__ work,
-                                                   uint32_t* __restrict__ work_count) {
-  constexpr int CAP = 8;
-  __shared__ uint32_t lds[Layout<CAP>::kWords * kWave];
-  const int lane = threadIdx.x;
-  const uint32_t g = blockIdx.x * kWave + lane;
-  const bool live = g < nblocks;
+#ifndef MYYUV_K2_WAVES
+#define MYYUV_K2_WAVES 1
+#endif
+__global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
+                                                         uint32_t nblocks,
+                                                         uint32_t* __restrict__ slots,
+                                                         uint8_t* __restrict__ sizes,
+                                                         uint32_t* __restrict__ work,
+                                                         uint32_t* __restrict__ work_count) {
+  constexpr int kWaves = kK2Group / kWave;
+  __shared__ uint32_t s_g[kK2Group];
+  __shared__ uint8_t s_msz[kK2Group], s_cls[kK2Group];
+  __shared__ uint32_t s_cnt[kWaves][kClassDead + 1];
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // ---- classify
+  const uint32_t g = blockIdx.x * kK2Group + tid;
+  uint32_t cls = kClassDead;
+  int msz = 0;
+  if (g < nblocks) {
+    CoefRegs R;
+    R.load(coef, g);
+    msz = R.msz();
+    cls = block_class(R, msz);
+  }
+  // ---- counting sort by class (stable: class, then wave, then lane)
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t rank = 0;
+#pragma unroll
+  for (uint32_t c = 0; c <= kClassDead; c++) {
+    const uint64_t b = __ballot(cls == c);
+    if (cls == c) rank = (uint32_t)__popcll(b & below);
+    if (lane == 0) s_cnt[wave][c] = (uint32_t)__popcll(b);
+  }
+  __syncthreads();
+  uint32_t pos = rank;
+#pragma unroll
+  for (uint32_t c = 0; c <= kClassDead; c++)
+#pragma unroll
+    for (uint32_t w = 0; w < (uint32_t)kWaves; w++)
+      pos += (c < cls || (c == cls && w < wave)) ? s_cnt[w][c] : 0u;
+  s_g[pos] = g;
+  s_msz[pos] = (uint8_t)msz;
+  s_cls[pos] = (uint8_t)cls;
+  __syncthreads();
+  // ---- encode: wave w takes sorted chunk w < kWaves/2 ? kWaves-1-w : w-kWaves/2
+  const uint32_t chunk = wave < (uint32_t)kWaves / 2 ? kWaves - 1 - wave : wave - kWaves / 2;
+  const uint32_t e = chunk * kWave + lane;
+  const uint32_t mg = s_g[e];
+  const int mm = s_msz[e];
+  const uint32_t mc = s_cls[e];
+  const bool live = mc != kClassDead;
+  uint32_t wcls = kClassDead;  // the wave's heaviest live class
+#pragma unroll
+  for (int c = kClassDead - 1; c >= 0; c--)
+    if (wcls == kClassDead && __ballot(mc == (uint32_t)c) != 0) wcls = (uint32_t)c;
+  if (wcls == kClassDead) return;
+  const int wmsz = max(wave_max(live ? mm : 0), 1);
+#ifdef MYYUV_STAMPS
+  if (lane == 0 && blockIdx.x * kWaves + wave < 8192) g_k2_fstamps[(blockIdx.x * kWaves + wave) * 8 + 0] = wcls | ((uint32_t)wmsz << 8);
+  const unsigned long long _w0 = __builtin_amdgcn_s_memtime();
+#endif
   CoefRegs R;
-  R.load(coef, g);  // the buffer spans whole waves: dead lanes read padding
-  const int msz = live ? R.msz() : 0;
-  const int wmsz = wave_max(msz);
-  const Img<CAP> I{lds, lane};
+  R.load(coef, live ? mg : 0u);
+  uint32_t* slot = slots + (size_t)(mg >> 6) * (kSlotWords * kWave) + (mg & 63);
+  uint8_t* so = sizes + mg;
   bool ok = true;
-  if (live)
-    ok = encode_block<CAP>(I, R, msz, max(wmsz, 1),
-                           slots + (size_t)blockIdx.x * (kSlotWords * kWave) + lane, sizes + g);
+  if (wcls == kClassSingle) {
+    if (live) encode_block_single(R, slot, so);
+  } else if (wcls == kClassR4) {
+    if (live) ok = encode_block_r<4>(R, mm, wmsz, slot, so);
+  } else {
+    if (live) ok = encode_block_r<8>(R, mm, wmsz, slot, so);
+  }
+#ifdef MYYUV_STAMPS
+  if (lane == 0 && blockIdx.x * kWaves + wave < 8192)
+    g_k2_fstamps[(blockIdx.x * kWaves + wave) * 8 + 7] = (uint32_t)(__builtin_amdgcn_s_memtime() - _w0);
+#endif
   const uint64_t ovf = __ballot(live && !ok);
   if (ovf) {
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(work_count, (uint32_t)__popcll(ovf));
     base = __builtin_amdgcn_readfirstlane(base);
-    if ((ovf >> lane) & 1) work[base + (uint32_t)__popcll(ovf & ((1ull << lane) - 1))] = g;
+    if ((ovf >> lane) & 1) work[base + (uint32_t)__popcll(ovf & below)] = mg;
   }
 }
 

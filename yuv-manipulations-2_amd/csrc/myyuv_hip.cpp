@@ -42,6 +42,7 @@ __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const S
 #ifdef MYYUV_STAMPS
 extern __device__ unsigned long long g_k2_stamps[40];
 extern __device__ uint32_t g_k2_wstamps[65536 * 8];
+extern __device__ uint32_t g_k2_fstamps[8192 * 8];
 #endif
 }  // namespace myyuv_gpu
 
@@ -262,7 +263,7 @@ int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, hipStream_t s) {
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
   if (hipMemsetAsync(count, 0, 4, s) != hipSuccess) return MYYUV_E_HIP;
-  int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(ceil_div(nblk, kWave)), dim3(kWave), s,
+  int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(ceil_div(nblk, kK2Group)), dim3(kK2Group), s,
                  c->coef.as<const uint4>(), nblk, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
                  list, count);
   e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
@@ -606,6 +607,18 @@ int myyuv_hip_kernel_stats(myyuv_hip_handle c, double ms[MYYUV_K_COUNT],
     launches[k] = c->launches[k];
   }
   return 0;
+}
+
+// Diagnostic builds: per-wave stage cycles of the CAP=8 pass (n waves).
+int myyuv_debug_k2_fstamps(uint32_t* out, uint32_t n) {
+#ifdef MYYUV_STAMPS
+  if (n > 8192) n = 8192;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_fstamps), (size_t)n * 32) == hipSuccess ? 0 : MYYUV_E_HIP;
+#else
+  (void)out;
+  (void)n;
+  return MYYUV_E_ARG;
+#endif
 }
 
 // Diagnostic builds: per-block phase cycles of the wave encoder (n blocks).
