@@ -110,13 +110,13 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
  * packet, as rocprofv3's kernel trace). */
 #define MYYUV_K_FDCT 0       /* K1 fdct_quant */
 #define MYYUV_K_HUFF_ENC 1   /* K2 huff_encode (CAP=8 pass over every block) */
-#define MYYUV_K_SCAN 2       /* scan of chunk sizes, per-tile pass (both directions) */
+#define MYYUV_K_SCAN 2       /* single-pass chunk-size scan (both directions; decode: + header checks) */
 #define MYYUV_K_COMPACT 3    /* K4 compaction into the DCTYUV stream */
-#define MYYUV_K_PARSE 4      /* decode-side stream header parse */
+#define MYYUV_K_PARSE 4      /* (unused: the header checks run inside MYYUV_K_SCAN) */
 #define MYYUV_K_HUFF_DEC 5   /* K5 huff_decode */
 #define MYYUV_K_IDCT 6       /* K6 dequant_idct */
 #define MYYUV_K_HUFF_WIDE 7  /* K2 overflow pass, lane per block (long worklists) */
-#define MYYUV_K_SCAN_SUMS 8  /* scan of chunk sizes, tile-prefix pass */
+#define MYYUV_K_SCAN_SUMS 8  /* (unused: the scan is single-pass) */
 #define MYYUV_K_HUFF_WAVE 9  /* K2 overflow pass, wave per block (short worklists) */
 #define MYYUV_K_COUNT 10
 int myyuv_hip_profile(myyuv_hip_handle h, int enable);

@@ -1,11 +1,10 @@
 // k_stream.hip — the variable-length side of the codec on gfx950:
-//   * k_scan_tiles / k_scan_sums: exclusive scan of the u8 chunk sizes
-//     (DCTYUVPlane::getContentPos, DCT.cpp:21-33, done for all planes at once);
+//   * k_scan_chain: exclusive scan of the u8 chunk sizes in one pass
+//     (DCTYUVPlane::getContentPos, DCT.cpp:21-33, done for all planes at once),
+//     decode side with the stream header checks;
 //   * k_compact: chunk slots -> the DCTYUV byte stream (DCTYUV::dump /
 //     DCTYUVPlane::dumpTo, DCT.cpp:63-73, 160-173, and the serial compaction of
 //     applyDCTPlane, :314-322);
-//   * k_parse: decode-side validation of the stream headers (DCTYUV::load,
-//     DCTYUVPlane::load, DCT.cpp:39-62, 130-159).
 //
 // Stream layout: u32 plane_size[3]; per plane p:
 //   u32 nblocks, u32 content_size, u8 chunk_size[nblocks], u8 content[...].
@@ -16,6 +15,7 @@
 //   header:  12 + 8p + cum[p] + off[cum[p]]
 // so one global scan places every byte of the stream.
 #include "codec_common.hpp"
+#include "k_chain.hpp"
 #include "k_stream.hpp"
 
 namespace myyuv_gpu {
@@ -42,20 +42,45 @@ __device__ __forceinline__ int plane_of(const uint32_t cum[4], uint32_t g) {
 
 }  // namespace
 
-// Exclusive scan inside tiles of kScanTile elements.  Element g's size byte is
-// src[pos[p] + (g - cum[p])] (pos: per-plane start of the u8 size array, read
-// from `desc` when given, so the decoder can scan sizes in place).
-__global__ __launch_bounds__(256) void k_scan_tiles(const uint8_t* __restrict__ src,
-                                                   ScanSrc S, const StreamDesc* __restrict__ desc,
+// Exclusive scan of the chunk sizes in one pass: workgroup t scans tile t
+// (kScanTile sizes) and finds the tile's exclusive prefix by decoupled
+// look-back over the lower tiles (k_chain.hpp); local_off[g] = offset inside
+// the tile, tile_pre[t] = the tile's prefix, tile_pre[ntiles] = the total.
+// Element g's size byte is src[pos[p] + (g - cum[p])].  With `desc` (decode)
+// every workgroup first parses the stream header (k_parse's checks, DCTYUV::load
+// DCT.cpp:130-159 then DCTYUVPlane::load :39-62) for the size positions, and
+// workgroup 0 publishes it for K5 (or records the header error).
+__global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ src, ScanSrc S,
+                                                   const uint32_t* __restrict__ in_size,
+                                                   uint32_t cap, FrameGeom G,
+                                                   StreamDesc* __restrict__ desc,
                                                    uint32_t* __restrict__ local_off,
-                                                   uint32_t* __restrict__ tile_sum) {
+                                                   uint32_t* __restrict__ tile_pre, uint32_t ntiles,
+                                                   unsigned long long* __restrict__ status,
+                                                   uint32_t epoch,
+                                                   unsigned long long* __restrict__ err) {
   __shared__ uint32_t wsum[4];
+  __shared__ uint32_t s_excl;
   uint32_t pos[3] = {S.pos[0], S.pos[1], S.pos[2]};
   if (desc) {
-    if (desc->bad) return;
-    pos[0] = desc->sizes_pos[0];
-    pos[1] = desc->sizes_pos[1];
-    pos[2] = desc->sizes_pos[2];
+    StreamPos P;
+    const int code = parse_stream(src, min(*in_size, cap), G, P);
+    if (code) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        desc->bad = 1;
+        record_error(err, 0, code);
+      }
+      return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      desc->bad = 0;
+      for (int p = 0; p < 3; p++) {
+        desc->sizes_pos[p] = P.sizes_pos[p];
+        desc->content_pos[p] = P.content_pos[p];
+        desc->content_size[p] = P.content_size[p];
+      }
+    }
+    for (int p = 0; p < 3; p++) pos[p] = P.sizes_pos[p];
   }
   const uint32_t base = blockIdx.x * kScanTile + threadIdx.x * kScanPerThread;
   uint32_t v[kScanPerThread];
@@ -75,6 +100,11 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const uint8_t* __restrict__ 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane == 63) wsum[wave] = incl;
   __syncthreads();
+  const uint32_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (wave == 0) {
+    const uint32_t ex = chained_prefix(status, blockIdx.x, 0, agg, epoch);
+    if (lane == 0) s_excl = ex;
+  }
   uint32_t carry = 0;
   for (int w = 0; w < wave; w++) carry += wsum[w];
   uint32_t run = carry + incl - sum;
@@ -84,31 +114,11 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const uint8_t* __restrict__ 
     if (g < S.cum[3]) local_off[g] = run;
     run += v[i];
   }
-  if (threadIdx.x == 255) tile_sum[blockIdx.x] = run;
-}
-
-// One workgroup: exclusive scan of the tile sums in place, total appended.
-__global__ __launch_bounds__(256) void k_scan_sums(uint32_t* __restrict__ tile_sum,
-                                                  uint32_t ntiles,
-                                                  const StreamDesc* __restrict__ desc) {
-  __shared__ uint32_t wsum[4];
-  if (desc && desc->bad) return;
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < ntiles; base += 256) {
-    const uint32_t i = base + threadIdx.x;
-    const uint32_t v = i < ntiles ? tile_sum[i] : 0;
-    const uint32_t incl = wave_inclusive_scan(v);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t c = carry;
-    for (int w = 0; w < wave; w++) c += wsum[w];
-    if (i < ntiles) tile_sum[i] = c + incl - v;
-    const uint32_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    __syncthreads();
-    carry += total;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tile_pre[blockIdx.x] = s_excl;
+    if (blockIdx.x == ntiles - 1) tile_pre[ntiles] = s_excl + agg;
   }
-  if (threadIdx.x == 0) tile_sum[ntiles] = carry;
 }
 
 __device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uint32_t* tile_pre,
@@ -195,57 +205,6 @@ __global__ __launch_bounds__(256) void k_compact(const uint32_t* __restrict__ sl
         if (b >= start && b < end) out[b] = (uint8_t)(w >> (8 * k));
       }
     }
-  }
-}
-
-// Decode-side header parse, one thread, in the reference's check order
-// (DCTYUV::load :130-159, then DCTYUVPlane::load :39-62 per plane).  Stricter
-// than the reference where it is undefined (see oracle_decompress).
-__global__ void k_parse(const uint8_t* __restrict__ in, const uint32_t* __restrict__ in_size,
-                        uint32_t cap, FrameGeom G, StreamDesc* __restrict__ desc,
-                        unsigned long long* __restrict__ err) {
-  if (threadIdx.x != 0) return;
-  auto rd32 = [&](uint64_t a) -> uint32_t {
-    return (uint32_t)in[a] | ((uint32_t)in[a + 1] << 8) | ((uint32_t)in[a + 2] << 16) |
-           ((uint32_t)in[a + 3] << 24);
-  };
-  int code = 0;
-  const uint32_t size = min(*in_size, cap);
-  uint32_t ps[3] = {0, 0, 0};
-  uint32_t hn[3] = {0, 0, 0}, hc[3] = {0, 0, 0};
-  uint64_t poff[3] = {12, 0, 0};
-  if (size <= 12) {
-    code = 6;
-  } else {
-    for (int p = 0; p < 3; p++) ps[p] = rd32(4 * p);
-    if (12ull + ps[0] + ps[1] + ps[2] > size) code = 6;
-  }
-  if (!code) {
-    poff[1] = poff[0] + ps[0];
-    poff[2] = poff[1] + ps[1];
-    for (int p = 0; p < 3 && !code; p++) {
-      if (ps[p] <= 8) { code = 7; break; }
-      hn[p] = rd32(poff[p]);
-      hc[p] = rd32(poff[p] + 4);
-      if (hn[p] == 0) code = 8;
-      else if (hc[p] == 0) code = 9;
-      else if (8ull + hn[p] + hc[p] > ps[p]) code = 7;
-    }
-  }
-  if (!code) {
-    for (int p = 0; p < 3 && !code; p++)
-      if (hn[p] < G.cum[p + 1] - G.cum[p]) code = 8;
-  }
-  if (code) {
-    desc->bad = 1;
-    record_error(err, 0, code);
-    return;
-  }
-  desc->bad = 0;
-  for (int p = 0; p < 3; p++) {
-    desc->sizes_pos[p] = (uint32_t)(poff[p] + 8);
-    desc->content_pos[p] = (uint32_t)(poff[p] + 8 + hn[p]);
-    desc->content_size[p] = hc[p];
   }
 }
 

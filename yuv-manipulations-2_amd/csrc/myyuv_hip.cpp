@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "codec_common.hpp"
+#include "k_chain.hpp"
 #include "k_stream.hpp"
 #include "myyuv_hip.h"
 
@@ -29,13 +30,12 @@ __global__ void k_huff_encode_wave(const uint4*, uint32_t*, uint8_t*, const uint
                                    const uint32_t*);
 __global__ void k_huff_encode_wide(const uint4*, uint32_t*, uint8_t*,
                                    const uint32_t*, const uint32_t*);
-__global__ void k_scan_tiles(const uint8_t*, ScanSrc, const StreamDesc*, uint32_t*, uint32_t*);
-__global__ void k_scan_sums(uint32_t*, uint32_t, const StreamDesc*);
+__global__ void k_scan_chain(const uint8_t*, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
+                             StreamDesc*, uint32_t*, uint32_t*, uint32_t, unsigned long long*,
+                             uint32_t, unsigned long long*);
 __global__ void k_compact(const uint32_t*, const uint8_t*, const uint32_t*, const uint32_t*,
                           FrameGeom, uint32_t, uint32_t, uint8_t*, uint32_t, uint32_t*,
                           unsigned long long*);
-__global__ void k_parse(const uint8_t*, const uint32_t*, uint32_t, FrameGeom, StreamDesc*,
-                        unsigned long long*);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
                               uint4*, unsigned long long*);
@@ -141,6 +141,10 @@ struct myyuv_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   DevBuf frame, coef, slots, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
+  // chained scan (k_chain.hpp): per-tile status words tagged with the launch
+  // epoch, counted here
+  DevBuf status;
+  uint32_t epoch = 0;
   // quantisation tables of the last quality triple (host copy; qtd on the
   // device, rewritten in stream order when the triple changes)
   QTables qt;
@@ -252,7 +256,18 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->psize.grow(4);
   e |= c->desc.grow(sizeof(StreamDesc));
   e |= c->work.grow((size_t)nblk * 4 + 256);  // [0]: overflow count, then block ids
+  const size_t st_bytes = (size_t)(ntiles + 1) * 8;
+  if (c->status.n < st_bytes) {
+    e |= c->status.grow(st_bytes);
+    if (!e && hipMemset(c->status.p, 0, st_bytes) != hipSuccess) e |= MYYUV_E_HIP;
+  }
   return e ? MYYUV_E_HIP : 0;
+}
+
+uint32_t next_epoch(myyuv_hip_ctx* c) {
+  c->epoch = (c->epoch + 1) & kEpochMask;
+  if (c->epoch == 0) c->epoch = 1;  // status words start zeroed: epoch 0 is never current
+  return c->epoch;
 }
 
 // K2: fast pass over all blocks, then the overflow pass over the blocks with
@@ -288,11 +303,9 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
   for (int p = 0; p < 3; p++) S.pos[p] = G.cum[p];
-  e |= launch(c, MYYUV_K_SCAN, k_scan_tiles, dim3(ntiles), dim3(256), s,
-              c->sizes.as<const uint8_t>(), S, (const StreamDesc*)nullptr, c->loff.as<uint32_t>(),
-              c->tiles.as<uint32_t>());
-  e |= launch(c, MYYUV_K_SCAN_SUMS, k_scan_sums, dim3(1), dim3(256), s, c->tiles.as<uint32_t>(),
-              ntiles, (const StreamDesc*)nullptr);
+  e |= launch(c, MYYUV_K_SCAN, k_scan_chain, dim3(ntiles), dim3(256), s, c->sizes.as<const uint8_t>(),
+              S, (const uint32_t*)nullptr, 0u, G, (StreamDesc*)nullptr, c->loff.as<uint32_t>(),
+              c->tiles.as<uint32_t>(), ntiles, c->status.as<unsigned long long>(), next_epoch(c), err);
   const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], 256), t1 = ceil_div(G.cum[2] - G.cum[1], 256),
                  t2 = ceil_div(G.cum[3] - G.cum[2], 256);
   e |= launch(c, MYYUV_K_COMPACT, k_compact, dim3(t0 + t1 + t2), dim3(256), s,
@@ -311,14 +324,12 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
   StreamDesc* desc = c->desc.as<StreamDesc>();
   const uint8_t* in = static_cast<const uint8_t*>(d_in);
   int e = 0;
-  e |= launch(c, MYYUV_K_PARSE, k_parse, dim3(1), dim3(64), s, in, d_size, cap, G, desc, err);
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
   for (int p = 0; p < 3; p++) S.pos[p] = 0;
-  e |= launch(c, MYYUV_K_SCAN, k_scan_tiles, dim3(ntiles), dim3(256), s, in, S,
-              (const StreamDesc*)desc, c->loff.as<uint32_t>(), c->tiles.as<uint32_t>());
-  e |= launch(c, MYYUV_K_SCAN_SUMS, k_scan_sums, dim3(1), dim3(256), s, c->tiles.as<uint32_t>(),
-              ntiles, (const StreamDesc*)desc);
+  e |= launch(c, MYYUV_K_SCAN, k_scan_chain, dim3(ntiles), dim3(256), s, in, S, d_size, cap, G, desc,
+              c->loff.as<uint32_t>(), c->tiles.as<uint32_t>(), ntiles,
+              c->status.as<unsigned long long>(), next_epoch(c), err);
   const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], kWave),
                  t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
@@ -346,7 +357,7 @@ int read_err(myyuv_hip_ctx* c, hipStream_t s, int64_t* bad_block) {
   return code;
 }
 
-// Host mirror of k_parse's header checks (same order), for host buffers.
+// Host mirror of the stream header checks (parse_stream, k_chain.hpp; same order), for host buffers.
 int host_parse_headers(const uint8_t* in, uint32_t size) {
   auto rd32 = [&](uint64_t a) {
     uint32_t v;
@@ -437,8 +448,8 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   (void)hipStreamSynchronize(c->stream);
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
-  DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff, &c->tiles,
-                    &c->payload, &c->err, &c->qtd,   &c->psize, &c->desc, &c->work};
+  DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff,  &c->tiles, &c->payload,
+                    &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -547,7 +558,7 @@ int myyuv_gpu_dct_decompress(myyuv_hip_handle c, const uint8_t* payload, uint32_
     if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
   // DCTYUV::load / DCTYUVPlane::load checks (DCT.cpp:454 -> :130-159, :39-62)
   // come before the dimension checks in the reference: validate the stream
-  // header on the host (the device re-checks it in k_parse).
+  // header on the host (the device re-checks it in k_scan_chain).
   if ((e_hdr = host_parse_headers(payload, size))) return e_hdr;
   FrameGeom G;
   int e = make_geom(w, h, G);
