@@ -6,9 +6,8 @@
  *  2. K1 quantisation: for every Q in 1..255 and every y within 256 ulps of
  *     each tie point h*Q (h a half-integer, |h*Q| <= 1100), plus random y in
  *     [-1100, 1100]: whenever the fast path's near-tie test says "far"
- *     (fma(e, e, W) < 0), its integer (low 16 bits of t + 1.5*2^23) equals
- *     (int)roundf(y / Q) — the reference's divide.  W is the per-lane
- *     threshold myyuv_hip.cpp builds: fma(1/Q, kNearScale, -0.25).
+ *     (fma(|t|, 2^-21, |e|) < 0.5), its integer (low 16 bits of
+ *     t + 1.5*2^23) equals (int)roundf(y / Q) — the reference's divide.
  *  3. K6 rounding: for s' in [-128, 127] near every half-integer and at
  *     random, when |s' - rint(s')| < 0.5 the low byte of s' + 1.5*2^23 + 128
  *     equals 128 + (int)roundf(s').
@@ -27,7 +26,7 @@ static uint32_t rnd(void) { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
 static const float kHalfDown = 0x1.fffffep-2f;
 static const float kMagic = 0x1.8p23f;
 static const float kMagicPx = 0x1.8p23f + 128.0f;
-static const float kNearScale = 2.0f * 1100.0f * 0x1p-21f;
+static const float kNearRel = 0x1p-21f;
 
 static int check_roundf(int all, uint64_t* n) {
   const uint64_t step = all ? 1 : 257;  /* a prime stride samples every exponent */
@@ -44,14 +43,13 @@ static int check_roundf(int all, uint64_t* n) {
 static int quant_one(float y, int Q, uint64_t* n) {
   const float q = (float)Q;
   const float r = 1.0f / q;
-  const float w = fmaf(r, kNearScale, -0.25f);
   volatile float t = y * r;
   volatile float u = t + kMagic;
   volatile float rt = u - kMagic;
   volatile float e = t - rt;
-  volatile float nt = fmaf(e, e, w);
+  volatile float nt = fmaf(fabsf(t), kNearRel, fabsf(e));
   (*n)++;
-  if (nt < 0.0f) {  /* fast path */
+  if (nt < 0.5f) {  /* fast path */
     const int16_t fast = (int16_t)(bits(u) & 0xFFFF);
     const int ref = (int)roundf(y / q);
     if (fast != (int16_t)ref) { printf("quant y=%a Q=%d fast=%d ref=%d\n", (double)y, Q, fast, ref); return 1; }

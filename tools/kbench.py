@@ -3,7 +3,9 @@
 the bench workload (chef-big 4032x3008 q50, HBM-resident) through
 compress_device + decompress_device, per-kernel HIP-event times.
 
-  MYYUV_HIP_LIB=<dir>/libmyyuv_hip.so python3 tools/kbench.py [steps]
+  MYYUV_HIP_LIB=<dir>/libmyyuv_hip.so python3 tools/kbench.py [steps] [WxH]
+
+WxH: a tiled synthetic frame of that size (SURVEY.md §8d generator) instead.
 """
 import os
 import sys
@@ -22,6 +24,11 @@ def main():
     g = myyuv_file.YUVFile.load(os.path.join(ROOT, "tests", "golden", "chef-with-trumpet-big-DCT-50.myyuv"))
     w, h, q = g.width, g.height, (50, 50, 50)
     raw = O.decompress(g.data, w, h, tuple(g.params))
+    if len(sys.argv) > 2:
+        import synth
+        ws, hs = w, h
+        w, h = (int(v) for v in sys.argv[2].split("x"))
+        raw = bytes(synth.tiled_frame(raw, ws, hs, w, h))
     expect = O.decompress(O.compress(raw, w, h, q), w, h, q)
     dev = torch.device("cuda", 0)
     codec = myyuv_hip.Codec(0)
@@ -44,7 +51,7 @@ def main():
             rc = repr(e)
     stats = codec.kernel_stats()
     ok = bytes(d_out.cpu().numpy()) == expect
-    print(f"{os.environ.get('MYYUV_HIP_LIB', 'default')}: rc={rc} roundtrip_equal={ok}")
+    print(f"{os.environ.get('MYYUV_HIP_LIB', 'default')} {w}x{h}: rc={rc} roundtrip_equal={ok}")
     for k, (ms, n) in stats.items():
         if n:
             print(f"  {k:14s} {ms / n * 1e3:9.2f} us")

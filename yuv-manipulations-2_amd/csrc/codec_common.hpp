@@ -8,6 +8,11 @@
 namespace myyuv_gpu {
 
 constexpr int kWave = 64;
+constexpr uint32_t kXfUnit = 16;  // blocks per K1/K6 wave unit (four lanes per block)
+#ifndef MYYUV_XF_WAVES
+#define MYYUV_XF_WAVES 8192
+#endif
+constexpr uint32_t kXfWaves = MYYUV_XF_WAVES;  // persistent K1/K6 grid: waves (8 per SIMD)
 constexpr int kSlotWords = 40;  // 160-B chunk slot per block (max chunk 155 B)
 constexpr int kMaxChunk = 160;
 
@@ -46,7 +51,7 @@ struct FrameGeom {
   uint32_t bw[3];         // blocks per block-row
   uint32_t cum[4];        // cumulative block counts: plane p owns [cum[p], cum[p+1])
   uint32_t poff[3];       // byte offset of plane p in the IYUV frame
-  uint32_t wcum[4];       // transform workgroups (64 blocks of one plane) per plane, cumulative
+  uint32_t ucum[4];       // transform units (kXfUnit blocks of one plane) per plane, cumulative
   uint64_t bmag[3];       // ceil(2^64 / bw[p]) (0 for bw = 1): block_row() divides by it
 };
 
@@ -61,18 +66,16 @@ __host__ __device__ __forceinline__ uint32_t block_row(const FrameGeom& G, int p
   return (uint32_t)(hi >> 32);
 }
 
-// Per-quality tables, passed to K1/K6 by value (kernel arguments).
+// Per-quality tables (a device buffer; K1/K6 stage q and r into LDS).
 struct QTables {
   float q[3][64];     // natural order, DCT.cpp:286-290
   float r[3][64];     // 1.0f / q, correctly rounded (K1's division-free fast path)
-  float near[3][4];   // K1 near-tie threshold of the lane owning rows 2j, 2j+1:
-                      // fma(max r over those rows, kNearScale, -0.25)
 };
 
-// 2 * Ymax * 2^-21 with Ymax = 1100 > the largest |Y| an 8x8 block of
-// x - 128 in [-128, 127] can produce (1024 at DC, < 850 elsewhere): K1's
-// near-tie window per unit of 1/Q (k_transform.hip).
-constexpr float kNearScale = 2.0f * 1100.0f * 0x1p-21f;
+// K1's near-tie window per unit of |t| (k_transform.hip): t = y * fl(1/Q)
+// may differ from fl(y / Q) by |t| * 1.5 * 2^-23; 2^-21 covers it with margin
+// (tools/check_numerics.c checks every Q at every tie; 2^-24 already fails).
+constexpr float kNearRel = 0x1p-21f;
 
 // Coefficient layout shared by K1, K2, K5 and K6: per block 64 int16 in
 // NATURAL (row-major) order, word w = coefficients 2w, 2w+1; words grouped in

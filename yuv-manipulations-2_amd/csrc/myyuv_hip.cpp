@@ -22,8 +22,8 @@
 #include "myyuv_hip.h"
 
 namespace myyuv_gpu {
-__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*);
-__global__ void k_dequant_idct(const uint4*, FrameGeom, const QTables*, uint8_t*);
+__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint4*);
+__global__ void k_dequant_idct(const uint4*, FrameGeom, const QTables*, uint8_t*, uint4*);
 __global__ void k_huff_encode(const uint4*, uint32_t, uint32_t*, uint8_t*,
                               uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, uint32_t*, uint8_t*, const uint32_t*,
@@ -69,14 +69,8 @@ void make_qtable(int q, bool chroma, float out[64]) {
 
 // Reciprocals and K1's per-lane near-tie thresholds from the Q tables.
 void finish_qtables(QTables& t, int planes) {
-  for (int p = 0; p < planes; p++) {
+  for (int p = 0; p < planes; p++)
     for (int n = 0; n < 64; n++) t.r[p][n] = 1.0f / t.q[p][n];
-    for (int j = 0; j < 4; j++) {
-      float rmax = 0.0f;
-      for (int n = 16 * j; n < 16 * j + 16; n++) rmax = std::max(rmax, t.r[p][n]);
-      t.near[p][j] = std::fma(rmax, kNearScale, -0.25f);
-    }
-  }
 }
 
 struct DevBuf {
@@ -106,6 +100,15 @@ constexpr uint8_t kZigzag[64] = MYYUV_ZIGZAG;
 
 uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
+// K1/K6 grid: persistent waves (four per 256-thread workgroup) striding over
+// the frame's 16-block units: as many workgroups as are resident at once
+// (`resident`, from the occupancy query at context creation), never more
+// waves than units.
+dim3 xf_grid(const FrameGeom& G, uint32_t resident) {
+  const uint32_t wgs = ceil_div(G.ucum[3], 4);
+  return dim3(wgs < resident ? wgs : resident);
+}
+
 // ceil(2^64 / bw) for FrameGeom::bmag; 0 marks bw = 1 (block_row returns local).
 uint64_t block_magic(uint32_t bw) { return bw > 1 ? ~0ull / bw + 1 : 0; }
 
@@ -127,7 +130,7 @@ int make_geom(uint32_t w, uint32_t h, FrameGeom& G) {
     G.bw[p] = pw[p] / 8;
     G.cum[p + 1] = G.cum[p] + G.bw[p] * (ph[p] / 8);
     G.bmag[p] = block_magic(G.bw[p]);
-    G.wcum[p + 1] = G.wcum[p] + ceil_div(G.cum[p + 1] - G.cum[p], kWave);
+    G.ucum[p + 1] = G.ucum[p] + ceil_div(G.cum[p + 1] - G.cum[p], kXfUnit);
   }
   G.poff[0] = 0;
   G.poff[1] = w * h;
@@ -141,6 +144,8 @@ struct myyuv_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   DevBuf frame, coef, slots, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
+  DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
+  uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
   // chained scan (k_chain.hpp): per-tile status words tagged with the launch
   // epoch, counted here
   DevBuf status;
@@ -253,6 +258,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->loff.grow((size_t)nblk * 4);
   e |= c->tiles.grow((size_t)(ntiles + 1) * 4);
   e |= c->err.grow(8);
+  e |= c->sink.grow(128 * 16);
   e |= c->psize.grow(4);
   e |= c->desc.grow(sizeof(StreamDesc));
   e |= c->work.grow((size_t)nblk * 4 + 256);  // [0]: overflow count, then block ids
@@ -297,8 +303,8 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   const QTables* qt = c->qtd.as<const QTables>();
   unsigned long long* err = c->err.as<unsigned long long>();
   int e = 0;
-  e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, dim3(G.wcum[3]), dim3(256), s,
-              static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>());
+  e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
+              static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->sink.as<uint4>());
   e |= launch_huff_encode(c, nblk, s);
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
@@ -336,8 +342,8 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
   e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2), dim3(kWave), s, in, d_size,
               cap, (const StreamDesc*)desc, c->loff.as<const uint32_t>(),
               c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<uint4>(), err);
-  e |= launch(c, MYYUV_K_IDCT, k_dequant_idct, dim3(G.wcum[3]), dim3(256), s,
-              c->coef.as<const uint4>(), G, qt, static_cast<uint8_t*>(d_out));
+  e |= launch(c, MYYUV_K_IDCT, k_dequant_idct, xf_grid(G, c->xf_resident[1]), dim3(256), s,
+              c->coef.as<const uint4>(), G, qt, static_cast<uint8_t*>(d_out), c->sink.as<uint4>());
   return e ? MYYUV_E_HIP : 0;
 }
 
@@ -432,6 +438,16 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
     delete c;
     return MYYUV_E_HIP;
   }
+  {
+    int cus = 0, n1 = 0, n6 = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n1, k_fdct_quant, 256, 0) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n6, k_dequant_idct, 256, 0) == hipSuccess &&
+        cus > 0 && n1 > 0 && n6 > 0) {
+      c->xf_resident[0] = (uint32_t)(cus * n1);
+      c->xf_resident[1] = (uint32_t)(cus * n6);
+    }
+  }
   if (c->err.grow(8) || c->psize.grow(4) || c->desc.grow(sizeof(StreamDesc)) ||
       hipMemset(c->err.p, 0xFF, 8) != hipSuccess) {
     (void)hipStreamDestroy(c->stream);
@@ -449,7 +465,7 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff,  &c->tiles, &c->payload,
-                    &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status};
+                    &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -691,7 +707,7 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
   G.bw[0] = 1;
   G.bmag[0] = block_magic(1);
   G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
-  G.wcum[1] = G.wcum[2] = G.wcum[3] = ceil_div(nblocks, kWave);
+  G.ucum[1] = G.ucum[2] = G.ucum[3] = ceil_div(nblocks, kXfUnit);
   QTables t;
   std::memset(&t, 0, sizeof(t));
   std::memcpy(t.q[0], qtable, 256);
@@ -703,8 +719,9 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
       hipMemcpy(c->qtd.p, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->frame.p, px, (size_t)nblocks * 64, hipMemcpyHostToDevice) != hipSuccess)
     return MYYUV_E_HIP;
-  hipLaunchKernelGGL(k_fdct_quant, dim3(G.wcum[3]), dim3(256), 0, s,
-                     c->frame.as<const uint8_t>(), G, c->qtd.as<const QTables>(), c->coef.as<uint4>());
+  hipLaunchKernelGGL(k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), 0, s,
+                     c->frame.as<const uint8_t>(), G, c->qtd.as<const QTables>(), c->coef.as<uint4>(),
+                     c->sink.as<uint4>());
   std::vector<uint32_t> words((size_t)ceil_div(nblocks, kWave) * kCoefQuadsPerWave * 4);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(words.data(), c->coef.p, words.size() * 4, hipMemcpyDeviceToHost, s) !=
