@@ -9,10 +9,16 @@ compressed stream resident in HBM: compress_device -> decompress_device on one
 stream.  value = megapixels (luma W*H) of all ranks' steps / max-over-ranks
 wall time of the K timed steps.
 
+Frames in flight (--inflight, default 3): step i runs on codec context i % 3,
+each context on its own HIP stream, so the latency-bound kernels of one frame
+(K2's overflow pass, the chained scans) overlap another frame's work.
+
 roofline: K1 fdct_quant (the block-transform kernel of the north star),
 algorithmic bytes = 3 B per sample (1 B u8 in + 2 B int16 out) x W*H*3/2
 samples per launch, divided by its average launch time from HIP events on the
-launch stream over the timed region.  `traffic` = FETCH_SIZE*2 + WRITE_SIZE
+launch stream over the timed region (where K1 shares the GPU with the other
+frames in flight); roofline_isolated: the same from the untimed one-frame-at-a-
+time breakdown pass.  `traffic` = FETCH_SIZE*2 + WRITE_SIZE
 per launch from a rocprofv3 --pmc run committed under profiles/ (null if none).
 
 cpu_baseline: the reference library itself (oracle/_ref, built from the
@@ -57,6 +63,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or nproc")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the step without K1's HIP events (no roofline)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="frames in flight per GPU: steps rotate over this many codec contexts, "
+                         "each on its own HIP stream, so one frame's latency-bound kernels overlap "
+                         "another's (1 = strictly serial)")
     ap.add_argument("--breakdown-steps", type=int, default=5,
                     help="untimed steps after the timed region with every kernel stamped")
     return ap.parse_args()
@@ -134,7 +144,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    codec = myyuv_hip.Codec(local)
+    nf = max(1, args.inflight)
+    codecs = [myyuv_hip.Codec(local) for _ in range(nf)]
+    codec = codecs[0]
 
     # ---- workload: the decoded big golden frame (sha-pinned)
     g = myyuv_file.YUVFile.load(GOLDEN_BIG)
@@ -145,45 +157,61 @@ def main():
     mp = w * h / 1e6
     samples = w * h * 3 // 2
     cap = myyuv_hip.payload_bound(w, h)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    # frame f runs on codec context f % nf and its own stream (contexts own
+    # their scratch buffers, so frames in flight never share one)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nf - 1)]
+    sps = [st.cuda_stream for st in streams]
     d_in = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
-    d_out = torch.empty(samples, dtype=torch.uint8, device=dev)
+    d_out = torch.empty((nf, samples), dtype=torch.uint8, device=dev)
     # one payload slot per timed step: the batch of compressed streams this
     # rank contributes (gathered to rank 0 at N>1)
-    nslot = max(1, args.steps)
+    nslot = max(nf, args.steps)
     d_pay = torch.empty((nslot, cap), dtype=torch.uint8, device=dev)
     d_size = torch.zeros(nslot, dtype=torch.int32, device=dev)
-    codec.reserve(w, h)
+    for c in codecs:
+        c.reserve(w, h)
 
     def step(i):
-        codec.compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay[i].data_ptr(), cap,
-                              d_size[i:i + 1].data_ptr(), sp)
-        codec.decompress_device(d_pay[i].data_ptr(), d_size[i:i + 1].data_ptr(), cap, w, h,
-                                (q, q, q), d_out.data_ptr(), sp)
+        k = i % nf
+        codecs[k].compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay[i].data_ptr(), cap,
+                                  d_size[i:i + 1].data_ptr(), sps[k])
+        codecs[k].decompress_device(d_pay[i].data_ptr(), d_size[i:i + 1].data_ptr(), cap, w, h,
+                                    (q, q, q), d_out[k].data_ptr(), sps[k])
 
-    for i in range(args.warmup):
+    def check_status():
+        for k, c in enumerate(codecs):
+            rc, bad = c.sync_status(sps[k])
+            if rc:
+                raise SystemExit(f"codec error {rc} ({myyuv_hip.strerror(rc)}) at block {bad}")
+
+    for i in range(max(args.warmup, nf)):
         step(i % nslot)
-    rc, bad = codec.sync_status(sp)
-    if rc:
-        raise SystemExit(f"codec error {rc} ({myyuv_hip.strerror(rc)}) at block {bad}")
+    check_status()
     n0 = int(d_size[0].item())
     pay0 = bytes(d_pay[0, :n0].cpu().numpy())
     if q == 50 and hashlib.sha256(pay0).hexdigest() != BIG_RECOMPRESSED_SHA:
         raise SystemExit("compressed stream differs from the pinned reference bytes")
-    if bytes(d_out.cpu().numpy()) != codec.decompress(pay0, w, h, (q, q, q)):
-        raise SystemExit("device round trip differs from the host-API decode")
+    host_rt = codec.decompress(pay0, w, h, (q, q, q))
+    for k in range(nf):
+        nk = int(d_size[k].item())
+        if bytes(d_pay[k, :nk].cpu().numpy()) != pay0:
+            raise SystemExit(f"context {k}: compressed stream differs from context 0's")
+        if bytes(d_out[k].cpu().numpy()) != host_rt:
+            raise SystemExit(f"context {k}: device round trip differs from the host-API decode")
 
     # ---- timed region: only K1 (the roofline kernel) is event-stamped, so the
     # other launches carry no profiling cost
     if not args.no_kernel_events:
-        codec.profile(True, kernels=["fdct_quant"])
+        for c in codecs:
+            c.profile(True, kernels=["fdct_quant"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i % nslot)
+    for st in streams[1:]:
+        streams[0].wait_stream(st)
     gathered = None
     if world > 1:
         # the batch's exchange step: every rank's compressed streams to rank 0
@@ -196,18 +224,25 @@ def main():
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
-    rc, bad = codec.sync_status(sp)
-    if rc:
-        raise SystemExit(f"codec error {rc} ({myyuv_hip.strerror(rc)}) at block {bad}")
-    stats = codec.kernel_stats() if not args.no_kernel_events else {}
-    codec.profile(False)
-    # per-kernel breakdown (all kernels stamped), outside the timed region
+    check_status()
+    stats = {}
+    if not args.no_kernel_events:
+        for c in codecs:
+            for kname, (kms, kn) in c.kernel_stats().items():
+                a, b = stats.get(kname, (0.0, 0))
+                stats[kname] = (a + kms, b + kn)
+            c.profile(False)
+    # per-kernel breakdown (all kernels stamped, one frame at a time), outside
+    # the timed region
     breakdown = {}
     if args.breakdown_steps > 0:
         codec.profile(True)
         for i in range(args.breakdown_steps):
-            step(i % nslot)
-        codec.sync_status(sp)
+            codec.compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay[i].data_ptr(), cap,
+                                  d_size[i:i + 1].data_ptr(), sps[0])
+            codec.decompress_device(d_pay[i].data_ptr(), d_size[i:i + 1].data_ptr(), cap, w, h,
+                                    (q, q, q), d_out[0].data_ptr(), sps[0])
+        codec.sync_status(sps[0])
         breakdown = codec.kernel_stats()
         codec.profile(False)
     if world > 1:
@@ -231,6 +266,13 @@ def main():
                     "traffic": load_traffic(), "kernel": "fdct_quant",
                     "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2)}
         kernel_us = {k: round(kms / kn * 1e3, 2) for k, (kms, kn) in breakdown.items() if kn}
+        # the same K1 figure with one frame at a time (the untimed breakdown
+        # pass): the kernel alone on the GPU, no co-running frame
+        roof_iso = None
+        if roof and kernel_us.get("fdct_quant"):
+            a_iso = 3 * samples / (kernel_us["fdct_quant"] * 1e-6) / 1e9
+            roof_iso = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
+                        "avg_launch_us": kernel_us["fdct_quant"]}
         for k, us in kernel_us.items():
             log(f"kernel {k:16s} {us:9.2f} us/launch")
         cpu = None
@@ -246,12 +288,13 @@ def main():
             "config": {"workload": f"chef-with-trumpet-big 4032x3008 IYUV DCT q={q} "
                                    f"compress+decompress, HBM-resident, 1 frame/step/GPU",
                        "frame": f"{w}x{h}", "quality": q, "parallelism": f"frames sharded, dp{world}",
-                       "payload_bytes": n0},
-            "roofline": roof, "cpu_baseline": cpu,
+                       "frames_in_flight": nf, "payload_bytes": n0},
+            "roofline": roof, "roofline_isolated": roof_iso, "cpu_baseline": cpu,
             "kernel_us": kernel_us or None,
         }
         print(json.dumps(line), flush=True)
-    codec.close()
+    for c in codecs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -235,7 +235,10 @@ __device__ __forceinline__ void load_quads(const uint4* __restrict__ coef, const
 // DCT.cpp:297-306 (gather, x - 128), :269-277 (applyDCTBlock).
 __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t* __restrict__ frame, FrameGeom G,
                                                    const QTables* __restrict__ qt,
-                                                   uint4* __restrict__ coef, uint4* __restrict__ sink) {
+                                                   uint4* __restrict__ coef, uint4* __restrict__ sink,
+                                                   uint32_t* __restrict__ k2ctl) {
+  // K2's overflow count for the launch that follows in the stream (nullptr: none)
+  if (k2ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *k2ctl = 0u;
   __shared__ float tile[4][kXfUnit * kTile];
   __shared__ float sqr[2 * 3 * 64];  // QTables::q then QTables::r
   static_assert(offsetof(QTables, r) == sizeof(float) * 3 * 64, "layout");

@@ -22,7 +22,7 @@
 #include "myyuv_hip.h"
 
 namespace myyuv_gpu {
-__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint4*);
+__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint4*, uint32_t*);
 __global__ void k_dequant_idct(const uint4*, FrameGeom, const QTables*, uint8_t*, uint4*);
 __global__ void k_huff_encode(const uint4*, uint32_t, uint32_t*, uint8_t*,
                               uint32_t*, uint32_t*);
@@ -265,7 +265,9 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   const size_t st_bytes = (size_t)(ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
-    if (!e && hipMemset(c->status.p, 0, st_bytes) != hipSuccess) e |= MYYUV_E_HIP;
+    // zeroed before any kernel on any stream reads it
+    if (!e && (hipMemset(c->status.p, 0, st_bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+      e |= MYYUV_E_HIP;
   }
   return e ? MYYUV_E_HIP : 0;
 }
@@ -283,7 +285,7 @@ uint32_t next_epoch(myyuv_hip_ctx* c) {
 int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, hipStream_t s) {
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
-  if (hipMemsetAsync(count, 0, 4, s) != hipSuccess) return MYYUV_E_HIP;
+  // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
   int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(ceil_div(nblk, kK2Group)), dim3(kK2Group), s,
                  c->coef.as<const uint4>(), nblk, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
                  list, count);
@@ -304,7 +306,8 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   unsigned long long* err = c->err.as<unsigned long long>();
   int e = 0;
   e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
-              static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->sink.as<uint4>());
+              static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->sink.as<uint4>(),
+              c->work.as<uint32_t>());
   e |= launch_huff_encode(c, nblk, s);
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
@@ -721,7 +724,7 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
     return MYYUV_E_HIP;
   hipLaunchKernelGGL(k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), 0, s,
                      c->frame.as<const uint8_t>(), G, c->qtd.as<const QTables>(), c->coef.as<uint4>(),
-                     c->sink.as<uint4>());
+                     c->sink.as<uint4>(), (uint32_t*)nullptr);
   std::vector<uint32_t> words((size_t)ceil_div(nblocks, kWave) * kCoefQuadsPerWave * 4);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(words.data(), c->coef.p, words.size() * 4, hipMemcpyDeviceToHost, s) !=
@@ -760,7 +763,8 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
     for (uint32_t c4 = 0; c4 < 8; c4++)
       std::memcpy(&words[(size_t)coef_quad(g, c4) * 4], nat + 8 * c4, 16);
   }
-  if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess)  // K1 zeroes it in the codec path
     return MYYUV_E_HIP;
   if (launch_huff_encode(c, nblocks, s)) return MYYUV_E_HIP;
   std::vector<uint32_t> slots((size_t)nwaves * kSlotWords * kWave);
