@@ -9,9 +9,13 @@ compressed stream resident in HBM: compress_device -> decompress_device on one
 stream.  value = megapixels (luma W*H) of all ranks' steps / max-over-ranks
 wall time of the K timed steps.
 
-Frames in flight (--inflight, default 3): step i runs on codec context i % 3,
-each context on its own HIP stream, so the latency-bound kernels of one frame
-(K2's overflow pass, the chained scans) overlap another frame's work.
+Batches and streams: a launch group of --batch frames (default 4) goes through
+the batch entry points (one launch per kernel for all of them: a 4K frame is
+too small to fill the MI355X, and every kernel's fixed launch and ramp time is
+shared), and --inflight groups (default 3) are in flight on their own codec
+contexts and HIP streams, so one group's latency-bound kernels (K2's overflow
+pass, the chained scans) overlap another's work.  A step is still one frame:
+value = frames x megapixels / wall time.
 
 roofline: K1 fdct_quant (the block-transform kernel of the north star),
 algorithmic bytes = 3 B per sample (1 B u8 in + 2 B int16 out) x W*H*3/2
@@ -55,7 +59,7 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--quality", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -67,6 +71,9 @@ def parse():
                     help="frames in flight per GPU: steps rotate over this many codec contexts, "
                          "each on its own HIP stream, so one frame's latency-bound kernels overlap "
                          "another's (1 = strictly serial)")
+    ap.add_argument("--batch", type=int, default=4,
+                    help="frames per launch (the batch entry points): each kernel covers this "
+                         "many frames")
     ap.add_argument("--breakdown-steps", type=int, default=5,
                     help="untimed steps after the timed region with every kernel stamped")
     return ap.parse_args()
@@ -157,26 +164,31 @@ def main():
     mp = w * h / 1e6
     samples = w * h * 3 // 2
     cap = myyuv_hip.payload_bound(w, h)
-    # frame f runs on codec context f % nf and its own stream (contexts own
-    # their scratch buffers, so frames in flight never share one)
+    # launch group j (frames j*B .. j*B+B-1) runs on codec context j % nf and
+    # its own stream (contexts own their scratch buffers, so groups in flight
+    # never share one)
+    B = max(1, args.batch)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nf - 1)]
     sps = [st.cuda_stream for st in streams]
-    d_in = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
-    d_out = torch.empty((nf, samples), dtype=torch.uint8, device=dev)
-    # one payload slot per timed step: the batch of compressed streams this
+    cap = (cap + 3) & ~3  # payload slots of a batch are dword aligned
+    d_in = torch.frombuffer(bytearray(raw * B), dtype=torch.uint8).to(dev)
+    d_out = torch.empty((nf, B * samples), dtype=torch.uint8, device=dev)
+    # one payload slot per timed frame: the batch of compressed streams this
     # rank contributes (gathered to rank 0 at N>1)
-    nslot = max(nf, args.steps)
+    ngroups = max(nf, (args.steps + B - 1) // B)
+    nslot = ngroups * B
     d_pay = torch.empty((nslot, cap), dtype=torch.uint8, device=dev)
     d_size = torch.zeros(nslot, dtype=torch.int32, device=dev)
     for c in codecs:
-        c.reserve(w, h)
+        c.reserve_batch(w, h, B)
 
-    def step(i):
-        k = i % nf
-        codecs[k].compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay[i].data_ptr(), cap,
-                                  d_size[i:i + 1].data_ptr(), sps[k])
-        codecs[k].decompress_device(d_pay[i].data_ptr(), d_size[i:i + 1].data_ptr(), cap, w, h,
-                                    (q, q, q), d_out[k].data_ptr(), sps[k])
+    def group(j, nb=B):
+        k = j % nf
+        f0 = (j % ngroups) * B
+        codecs[k].compress_batch_device(d_in.data_ptr(), nb, w, h, (q, q, q), d_pay[f0].data_ptr(), cap,
+                                        d_size[f0:f0 + nb].data_ptr(), sps[k])
+        codecs[k].decompress_batch_device(d_pay[f0].data_ptr(), d_size[f0:f0 + nb].data_ptr(), cap, nb,
+                                          w, h, (q, q, q), d_out[k].data_ptr(), sps[k])
 
     def check_status():
         for k, c in enumerate(codecs):
@@ -184,20 +196,22 @@ def main():
             if rc:
                 raise SystemExit(f"codec error {rc} ({myyuv_hip.strerror(rc)}) at block {bad}")
 
-    for i in range(max(args.warmup, nf)):
-        step(i % nslot)
+    for j in range(max(args.warmup // B, nf)):
+        group(j)
     check_status()
     n0 = int(d_size[0].item())
     pay0 = bytes(d_pay[0, :n0].cpu().numpy())
     if q == 50 and hashlib.sha256(pay0).hexdigest() != BIG_RECOMPRESSED_SHA:
         raise SystemExit("compressed stream differs from the pinned reference bytes")
     host_rt = codec.decompress(pay0, w, h, (q, q, q))
+    for f in range(nf * B):
+        nk = int(d_size[f].item())
+        if bytes(d_pay[f, :nk].cpu().numpy()) != pay0:
+            raise SystemExit(f"frame slot {f}: compressed stream differs from slot 0's")
     for k in range(nf):
-        nk = int(d_size[k].item())
-        if bytes(d_pay[k, :nk].cpu().numpy()) != pay0:
-            raise SystemExit(f"context {k}: compressed stream differs from context 0's")
-        if bytes(d_out[k].cpu().numpy()) != host_rt:
-            raise SystemExit(f"context {k}: device round trip differs from the host-API decode")
+        for b in range(B):
+            if bytes(d_out[k, b * samples:(b + 1) * samples].cpu().numpy()) != host_rt:
+                raise SystemExit(f"context {k} frame {b}: device round trip differs from the host-API decode")
 
     # ---- timed region: only K1 (the roofline kernel) is event-stamped, so the
     # other launches carry no profiling cost
@@ -208,8 +222,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i % nslot)
+    for j in range((args.steps + B - 1) // B):  # the last group takes the remainder
+        group(j, min(B, args.steps - j * B))
     for st in streams[1:]:
         streams[0].wait_stream(st)
     gathered = None
@@ -232,16 +246,13 @@ def main():
                 a, b = stats.get(kname, (0.0, 0))
                 stats[kname] = (a + kms, b + kn)
             c.profile(False)
-    # per-kernel breakdown (all kernels stamped, one frame at a time), outside
-    # the timed region
+    # per-kernel breakdown (all kernels stamped, one launch group at a time on
+    # one stream), outside the timed region
     breakdown = {}
     if args.breakdown_steps > 0:
         codec.profile(True)
         for i in range(args.breakdown_steps):
-            codec.compress_device(d_in.data_ptr(), w, h, (q, q, q), d_pay[i].data_ptr(), cap,
-                                  d_size[i:i + 1].data_ptr(), sps[0])
-            codec.decompress_device(d_pay[i].data_ptr(), d_size[i:i + 1].data_ptr(), cap, w, h,
-                                    (q, q, q), d_out[0].data_ptr(), sps[0])
+            group(0)
         codec.sync_status(sps[0])
         breakdown = codec.kernel_stats()
         codec.profile(False)
@@ -259,18 +270,18 @@ def main():
         roof = None
         if k1_n:
             avg_s = k1_ms / k1_n / 1e3
-            alg = 3 * samples
+            alg = round(3 * samples * args.steps / k1_n)  # a launch covers a batch of frames
             achieved = alg / avg_s / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": load_traffic(), "kernel": "fdct_quant",
                     "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2)}
         kernel_us = {k: round(kms / kn * 1e3, 2) for k, (kms, kn) in breakdown.items() if kn}
-        # the same K1 figure with one frame at a time (the untimed breakdown
-        # pass): the kernel alone on the GPU, no co-running frame
+        # the same K1 figure with one launch group at a time (the untimed
+        # breakdown pass): the kernel alone on the GPU, no co-running group
         roof_iso = None
         if roof and kernel_us.get("fdct_quant"):
-            a_iso = 3 * samples / (kernel_us["fdct_quant"] * 1e-6) / 1e9
+            a_iso = 3 * samples * B / (kernel_us["fdct_quant"] * 1e-6) / 1e9
             roof_iso = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
                         "avg_launch_us": kernel_us["fdct_quant"]}
         for k, us in kernel_us.items():
@@ -288,7 +299,7 @@ def main():
             "config": {"workload": f"chef-with-trumpet-big 4032x3008 IYUV DCT q={q} "
                                    f"compress+decompress, HBM-resident, 1 frame/step/GPU",
                        "frame": f"{w}x{h}", "quality": q, "parallelism": f"frames sharded, dp{world}",
-                       "frames_in_flight": nf, "payload_bytes": n0},
+                       "launch_groups_in_flight": nf, "frames_per_launch": B, "payload_bytes": n0},
             "roofline": roof, "roofline_isolated": roof_iso, "cpu_baseline": cpu,
             "kernel_us": kernel_us or None,
         }

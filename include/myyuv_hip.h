@@ -99,6 +99,23 @@ int myyuv_gpu_dct_decompress_device(myyuv_hip_handle h, const void* d_payload,
                                     const uint32_t* d_payload_size, uint32_t cap, uint32_t width,
                                     uint32_t height, const uint8_t quality[3], void* d_iyuv,
                                     void* stream);
+/* Batches: `nframes` frames of one geometry per launch of each kernel (the
+ * batch configuration of SURVEY.md §8d; fills the GPU where one 4K frame
+ * cannot).  Frame f at d_iyuv + f*W*H*3/2; payload f at d_payload + f*cap
+ * (cap a multiple of 4 when nframes > 1), its size at d_payload_sizes[f].
+ * A device-side error reports the batch-global block index
+ * (f * blocks_per_frame + block) of the first failing block; a header error
+ * of frame f > 0 reports f * blocks_per_frame.  Each frame's bytes are those
+ * of the single-frame call. */
+int myyuv_hip_reserve_batch(myyuv_hip_handle h, uint32_t width, uint32_t height, uint32_t nframes);
+int myyuv_gpu_dct_compress_batch_device(myyuv_hip_handle h, const void* d_iyuv, uint32_t nframes,
+                                        uint32_t width, uint32_t height, const uint8_t quality[3],
+                                        void* d_payload, uint32_t cap, uint32_t* d_payload_sizes,
+                                        void* stream);
+int myyuv_gpu_dct_decompress_batch_device(myyuv_hip_handle h, const void* d_payload,
+                                          const uint32_t* d_payload_sizes, uint32_t cap,
+                                          uint32_t nframes, uint32_t width, uint32_t height,
+                                          const uint8_t quality[3], void* d_iyuv, void* stream);
 /* Waits for `stream`, returns (and clears) the first device-side error since
  * the last call; *bad_block as above. */
 int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);

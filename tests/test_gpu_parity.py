@@ -217,3 +217,90 @@ def test_irregular_tables_match_oracle(codec, oracle, wh):
         exp = oracle.decompress(p, w, h, (q, q, q))
         assert exp != oracle.decompress(pay, w, h, (q, q, q)), name
         assert codec.decompress(p, w, h, (q, q, q)) == exp, name
+
+
+def _batch_frames(golden, w, h, n):
+    """n distinct frames of one geometry: the chef-small frame, tiled shifts
+    of it (SURVEY.md §8d generator) and a noise frame."""
+    import synth
+    raw = golden("chef-with-trumpet.myyuv").data
+    frames = []
+    for f in range(n):
+        if f % 3 == 2:
+            frames.append(synth.noise_frame(w, h, seed=77 + f).tobytes())
+        else:
+            ox, oy = synth.batch_origin(f, SMALL_W, SMALL_H)
+            frames.append(bytes(synth.tiled_frame(raw, SMALL_W, SMALL_H, w, h, ox, oy)))
+    return frames
+
+
+@pytest.mark.parametrize("wh,n,q", [((992, 736), 3, (50, 50, 50)), ((144, 272), 5, (90, 40, 75)),
+                                    ((1008, 16), 2, (1, 100, 50))])
+def test_batch_device_matches_single_frames(codec, oracle, golden, wh, n, q):
+    """One launch per kernel over n frames (blocks numbered across the batch,
+    per-frame scans and output slots): every payload and every decoded frame
+    equals the oracle's single-frame result."""
+    import torch
+    import myyuv_hip
+    w, h = wh
+    frames = _batch_frames(golden, w, h, n)
+    fb = w * h * 3 // 2
+    cap = (myyuv_hip.payload_bound(w, h) + 3) & ~3
+    d_in = torch.frombuffer(bytearray(b"".join(frames)), dtype=torch.uint8).cuda()
+    d_pay = torch.zeros(n * cap, dtype=torch.uint8, device="cuda")
+    d_sizes = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_out = torch.empty(n * fb, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    codec.reserve_batch(w, h, n)
+    for _ in range(2):  # twice: nothing may depend on a fresh workspace
+        codec.compress_batch_device(d_in.data_ptr(), n, w, h, q, d_pay.data_ptr(), cap,
+                                    d_sizes.data_ptr(), stream)
+        codec.decompress_batch_device(d_pay.data_ptr(), d_sizes.data_ptr(), cap, n, w, h, q,
+                                      d_out.data_ptr(), stream)
+        rc, bad = codec.sync_status(stream)
+        assert rc == 0, (rc, bad)
+        pay = d_pay.cpu().numpy()
+        out = d_out.cpu().numpy()
+        sizes = d_sizes.cpu().numpy()
+        for f in range(n):
+            exp = oracle.compress(frames[f], w, h, q)
+            got = bytes(pay[f * cap: f * cap + int(sizes[f])])
+            assert got == exp, f
+            assert bytes(out[f * fb:(f + 1) * fb]) == oracle.decompress(exp, w, h, q), f
+
+
+def test_batch_decode_error_reports_frame(codec, oracle, golden):
+    """A malformed chunk in frame 1 of a batch: the reference's error, at the
+    batch-global index of the failing block (frame 1 * blocks per frame + block)."""
+    import torch
+    import malformed
+    import myyuv_hip
+    g = golden("chef-with-trumpet-DCT-50.myyuv")
+    w, h, q = g.width, g.height, tuple(g.params)
+    nblk = (w // 8) * (h // 8) + 2 * (w // 16) * (h // 16)
+    name, badpay = next((n, p) for n, p, kind in malformed.cases(g.data) if n == "bad_code")
+    try:
+        oracle.decompress(badpay, w, h, q)
+        raise AssertionError("oracle accepted " + name)
+    except RuntimeError as e:
+        exp_code = e.args[0]
+    single_bad = None
+    try:
+        codec.decompress(badpay, w, h, q)
+    except myyuv_hip.CodecError as e:
+        assert e.code == exp_code
+        single_bad = e.bad_block
+    assert single_bad is not None and single_bad >= 0
+    cap = (max(len(g.data), len(badpay)) + 3) & ~3
+    buf = bytearray(2 * cap)
+    buf[:len(g.data)] = g.data
+    buf[cap:cap + len(badpay)] = badpay
+    d_pay = torch.frombuffer(buf, dtype=torch.uint8).cuda()
+    d_sizes = torch.tensor([len(g.data), len(badpay)], dtype=torch.int32, device="cuda")
+    d_out = torch.empty(2 * w * h * 3 // 2, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    codec.decompress_batch_device(d_pay.data_ptr(), d_sizes.data_ptr(), cap, 2, w, h, q,
+                                  d_out.data_ptr(), stream)
+    rc, bad = codec.sync_status(stream)
+    assert rc == exp_code
+    assert bad == nblk + single_bad

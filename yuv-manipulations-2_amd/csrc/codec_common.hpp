@@ -53,17 +53,28 @@ struct FrameGeom {
   uint32_t poff[3];       // byte offset of plane p in the IYUV frame
   uint32_t ucum[4];       // transform units (kXfUnit blocks of one plane) per plane, cumulative
   uint64_t bmag[3];       // ceil(2^64 / bw[p]) (0 for bw = 1): block_row() divides by it
+  // A batch of `nframes` frames of this geometry, frame f at byte f * fbytes
+  // of the frame buffer; its blocks are numbered f * cum[3] + g (batch-global)
+  // in the coefficient, slot and size buffers.
+  uint32_t nframes;
+  uint32_t fbytes;        // W * H * 3 / 2
+  uint64_t umag;          // ceil(2^64 / ucum[3]) (0 for 1 unit): batch unit -> frame
 };
+
+// floor(x / d) for a 32-bit x from m = ceil(2^64 / d) (m = 0 for d = 1): the
+// product overshoots x / d by less than x / 2^64, below the 1 / d slack.
+__host__ __device__ __forceinline__ uint32_t div_magic(uint32_t x, uint64_t m) {
+  if (m == 0) return x;
+  const uint64_t lo = (uint64_t)x * (uint32_t)m;
+  const uint64_t hi = (uint64_t)x * (uint32_t)(m >> 32) + (lo >> 32);
+  return (uint32_t)(hi >> 32);
+}
 
 // by = floor(local / bw) = high 64 bits of local * ceil(2^64 / bw): the
 // product overshoots local / bw by less than local / 2^64, below the 1 / bw
 // slack, so the floor is exact for every 32-bit local.
 __host__ __device__ __forceinline__ uint32_t block_row(const FrameGeom& G, int p, uint32_t local) {
-  const uint64_t m = G.bmag[p];
-  if (m == 0) return local;
-  const uint64_t lo = (uint64_t)local * (uint32_t)m;
-  const uint64_t hi = (uint64_t)local * (uint32_t)(m >> 32) + (lo >> 32);
-  return (uint32_t)(hi >> 32);
+  return div_magic(local, G.bmag[p]);
 }
 
 // Per-quality tables (a device buffer; K1/K6 stage q and r into LDS).
@@ -90,7 +101,10 @@ constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
 
 // K2 overflow worklists up to this many blocks are encoded wave-per-block
 // (k_huff_encode_wave), longer ones lane-per-block (k_huff_encode_wide).
-constexpr uint32_t kWaveEncodeLimit = 24576;
+#ifndef MYYUV_WAVE_LIMIT
+#define MYYUV_WAVE_LIMIT 24576
+#endif
+constexpr uint32_t kWaveEncodeLimit = MYYUV_WAVE_LIMIT;
 constexpr uint32_t kWaveEncodeGrid = 16384;  // waves of k_huff_encode_wave
 #ifndef MYYUV_K2_GROUP
 #define MYYUV_K2_GROUP 256

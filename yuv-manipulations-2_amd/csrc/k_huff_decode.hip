@@ -286,6 +286,15 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
                                                    uint4* __restrict__ coef,
                                                    unsigned long long* __restrict__ err) {
   __shared__ uint4 stq[kStageQuads];
+  // frame blockIdx.y of the batch: its stream slot, descriptor and scan;
+  // coefficients at batch-global block gbase + g
+  const uint32_t f = blockIdx.y;
+  const uint32_t gbase = f * G.cum[3];
+  const uint32_t ntiles = (G.cum[3] + kScanTile - 1) / kScanTile;
+  in += (size_t)f * cap;
+  desc += f;
+  local_off += gbase;
+  tile_pre += (size_t)f * (ntiles + 1);
   if (desc->bad) return;
   const int lane = threadIdx.x;
   const uint32_t t = blockIdx.x;
@@ -295,7 +304,7 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
   const uint32_t g1 = min(g0 + kWave, G.cum[p + 1]);
   const uint32_t g = g0 + lane;
   const bool live = g < g1;
-  const uint32_t limit = min(*in_size, cap);
+  const uint32_t limit = min(in_size[f], cap);
   const uint32_t nblk = G.cum[3];
 
   // end of the wave's chunk range from the scan alone (rel(nblk) = the total)
@@ -313,7 +322,7 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
   // the chunks must fit the declared content.
   bool ok = live;
   if (live && rel + s > csize) {
-    record_error(err, 2ull * G.cum[p], 9 /* MYYUV_E_PLANE_CONTENT */);
+    record_error(err, 2ull * (gbase + G.cum[p]), 9 /* MYYUV_E_PLANE_CONTENT */);
     ok = false;
   }
 
@@ -386,19 +395,19 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
 #endif
     if (go && !T.regular) {
       direct = true;
-      dcode = decode_general(lc, T, coef, g);
+      dcode = decode_general(lc, T, coef, gbase + g);
     }
     if (mine) code = go ? dcode : pcode;
     pending &= ~__ballot(mine);
     __syncthreads();  // the next round overwrites the stage
   }
-  if (ok && code) record_error(err, 2ull * g + 1, code);
+  if (ok && code) record_error(err, 2ull * (gbase + g) + 1, code);
 
   // ---- natural-order words to the quad layout (1 KiB contiguous per store)
   if (live && !direct) {
 #pragma unroll
     for (int c = 0; c < 8; c++)
-      coef[coef_quad(g, c)] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
+      coef[coef_quad(gbase + g, c)] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
   }
 }
 

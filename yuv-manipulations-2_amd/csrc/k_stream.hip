@@ -42,7 +42,8 @@ __device__ __forceinline__ int plane_of(const uint32_t cum[4], uint32_t g) {
 
 }  // namespace
 
-// Exclusive scan of the chunk sizes in one pass: workgroup t scans tile t
+// Exclusive scan of the chunk sizes in one pass (frame blockIdx.y of a batch,
+// its bytes at src + blockIdx.y * src_stride): workgroup t scans tile t
 // (kScanTile sizes) and finds the tile's exclusive prefix by decoupled
 // look-back over the lower tiles (k_chain.hpp); local_off[g] = offset inside
 // the tile, tile_pre[t] = the tile's prefix, tile_pre[ntiles] = the total.
@@ -50,8 +51,8 @@ __device__ __forceinline__ int plane_of(const uint32_t cum[4], uint32_t g) {
 // every workgroup first parses the stream header (k_parse's checks, DCTYUV::load
 // DCT.cpp:130-159 then DCTYUVPlane::load :39-62) for the size positions, and
 // workgroup 0 publishes it for K5 (or records the header error).
-__global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ src, ScanSrc S,
-                                                   const uint32_t* __restrict__ in_size,
+__global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ src, uint32_t src_stride,
+                                                   ScanSrc S, const uint32_t* __restrict__ in_size,
                                                    uint32_t cap, FrameGeom G,
                                                    StreamDesc* __restrict__ desc,
                                                    uint32_t* __restrict__ local_off,
@@ -61,14 +62,22 @@ __global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ 
                                                    unsigned long long* __restrict__ err) {
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t s_excl;
+  // frame blockIdx.y of the batch: its own sizes / stream, offsets, tile
+  // prefixes and look-back chain
+  const uint32_t f = blockIdx.y;
+  src += (size_t)f * src_stride;
+  local_off += (size_t)f * G.cum[3];
+  tile_pre += (size_t)f * (ntiles + 1);
+  status += (size_t)f * (ntiles + 1);
   uint32_t pos[3] = {S.pos[0], S.pos[1], S.pos[2]};
   if (desc) {
+    desc += f;
     StreamPos P;
-    const int code = parse_stream(src, min(*in_size, cap), G, P);
+    const int code = parse_stream(src, min(in_size[f], cap), G, P);
     if (code) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         desc->bad = 1;
-        record_error(err, 0, code);
+        record_error(err, 2ull * f * G.cum[3], code);  // frame f's first block (0: header of frame 0)
       }
       return;
     }
@@ -126,7 +135,8 @@ __device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uin
   return local_off[g] + tile_pre[g / kScanTile];
 }
 
-// Compaction: one workgroup = up to 256 consecutive blocks of one plane.
+// Compaction: one workgroup = up to 256 consecutive blocks of one plane of
+// frame blockIdx.y.
 // Chunks are OR-ed into an LDS image aligned to the stream's dword grid, then
 // written with dword stores (edge words byte by byte: they are shared with the
 // neighbouring workgroups' bytes).
@@ -139,6 +149,15 @@ __global__ __launch_bounds__(256) void k_compact(const uint32_t* __restrict__ sl
                                                 uint32_t* __restrict__ out_size,
                                                 unsigned long long* __restrict__ err) {
   __shared__ uint32_t img[(256 * kMaxChunk) / 4 + 2];
+  // frame blockIdx.y of the batch: slots / sizes at batch-global block
+  // gbase + g, its scan, its output slot of `cap` bytes
+  const uint32_t f = blockIdx.y, gbase = f * G.cum[3];
+  const uint32_t ntiles = (G.cum[3] + kScanTile - 1) / kScanTile;
+  sizes += gbase;
+  local_off += gbase;
+  tile_pre += (size_t)f * (ntiles + 1);
+  out += (size_t)f * cap;
+  out_size += f;
   const uint32_t t = blockIdx.x;
   const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
   const uint32_t tile_in_plane = t - (p == 0 ? 0 : (p == 1 ? tiles_p0 : tiles_p0 + tiles_p1));
@@ -162,7 +181,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint32_t* __restrict__ sl
     }
     if (p == 0 && threadIdx.x == 1) {
       *out_size = (uint32_t)total;
-      if (total > cap) record_error(err, 0, 5 /* MYYUV_E_CAPACITY */);
+      if (total > cap) record_error(err, 0, 5 /* MYYUV_E_CAPACITY */);  // any frame
     }
   }
   if (total > cap) return;
@@ -183,7 +202,8 @@ __global__ __launch_bounds__(256) void k_compact(const uint32_t* __restrict__ sl
     const uint32_t s = sizes[g];
     out[12ull + 8ull * (p + 1) + plane_pre + g] = (uint8_t)s;  // chunk_size[k]
     const uint32_t lo = (uint32_t)(start - astart) + (scanned(local_off, tile_pre, g) - off0);
-    const uint32_t* slot = slots + (size_t)(g / kWave) * (kSlotWords * kWave) + (g % kWave);
+    const uint32_t ga = gbase + g;
+    const uint32_t* slot = slots + (size_t)(ga / kWave) * (kSlotWords * kWave) + (ga % kWave);
     const uint32_t nw = (s + 3) >> 2;
     const uint32_t sh = (lo & 3) * 8;
     for (uint32_t j = 0; j < nw; j++) {

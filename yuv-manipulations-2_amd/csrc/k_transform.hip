@@ -34,6 +34,8 @@
 // block's pixel rows 2q, 2q+1 directly (8 B each; 16 blocks x 8 B = 128 B
 // runs per row) and its two coefficient quads 2q, 2q+1 (codec_common.hpp
 // layout; 256 B runs).  The per-quality tables (QTables) are a device buffer.
+// A launch covers a batch of frames (FrameGeom::nframes): the waves stride
+// over the units of all of them, frame f's unit u being f * ucum[3] + u.
 //
 // Bit-exactness (SURVEY.md §7 hard part 1, App. C): each output is the
 // reference's straight k-ascending sum of fp32-rounded products
@@ -199,12 +201,14 @@ __device__ __forceinline__ float sbyte(uint32_t w, int k) {  // byte k of w, sig
 // results go to the sink): the loads are unconditional and their values are
 // not touched until the next iteration, so the wave does not wait for them.
 __device__ __forceinline__ uint4 load_rows(const uint8_t* __restrict__ frame, const FrameGeom& G,
-                                           uint32_t u, uint32_t b, uint32_t q) {
-  const Unit U = unit_of(G, u);
+                                           uint32_t ua, uint32_t b, uint32_t q) {
+  const uint32_t f = div_magic(ua, G.umag);
+  const Unit U = unit_of(G, ua - f * G.ucum[3]);
   const uint32_t local = U.local0 + b;
   const uint32_t off = block_row_offset(U, local < U.nb ? local : U.nb - 1, 2u * q);
-  const uint2 r0 = *reinterpret_cast<const uint2*>(frame + off);
-  const uint2 r1 = *reinterpret_cast<const uint2*>(frame + off + U.pw);
+  const uint8_t* fr = frame + (size_t)f * G.fbytes;
+  const uint2 r0 = *reinterpret_cast<const uint2*>(fr + off);
+  const uint2 r1 = *reinterpret_cast<const uint2*>(fr + off + U.pw);
   return make_uint4(r0.x, r0.y, r1.x, r1.y);
 }
 
@@ -221,10 +225,11 @@ __device__ __forceinline__ void stage_tables(const float* __restrict__ src, floa
 // Coefficient quads 2q, 2q+1 (rows 2q, 2q+1) of the lane's block in unit u
 // (the last block of the plane past its end).
 __device__ __forceinline__ void load_quads(const uint4* __restrict__ coef, const FrameGeom& G,
-                                           uint32_t u, uint32_t b, uint32_t q, uint4& a, uint4& c) {
-  const Unit U = unit_of(G, u);
+                                           uint32_t ua, uint32_t b, uint32_t q, uint4& a, uint4& c) {
+  const uint32_t f = div_magic(ua, G.umag);
+  const Unit U = unit_of(G, ua - f * G.ucum[3]);
   const uint32_t local = U.local0 + b;
-  const uint32_t g = U.cum + (local < U.nb ? local : U.nb - 1);
+  const uint32_t g = f * G.cum[3] + U.cum + (local < U.nb ? local : U.nb - 1);
   a = coef[coef_quad(g, 2 * q)];
   c = coef[coef_quad(g, 2 * q + 1)];
 }
@@ -247,19 +252,21 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
   const uint32_t q = lane & 3u, b = lane >> 2;  // quarter, block in the unit
   float* tb = tile[threadIdx.x >> 6] + b * kTile;
   uint8_t* img = reinterpret_cast<uint8_t*>(tb);  // the block's 8 x 8 B pixel image (aliases tb)
-  const uint32_t nu = G.ucum[3], stride = unit_stride();
-  uint32_t u = first_unit();
-  uint4 nx = u < nu ? load_rows(frame, G, u, b, q) : make_uint4(0, 0, 0, 0);
+  // batch units: unit u of frame f is ua = f * ucum[3] + u
+  const uint32_t nall = G.ucum[3] * G.nframes, stride = unit_stride();
+  uint32_t ua = first_unit();
+  uint4 nx = ua < nall ? load_rows(frame, G, ua, b, q) : make_uint4(0, 0, 0, 0);
   // two stores behind the first loads, as every iteration has behind its
   // prefetch: the loop top then waits with vmcnt(2) on every path
   sink[lane] = make_uint4(0, 0, 0, 0);
   sink[64 + lane] = make_uint4(0, 0, 0, 0);
 
-  for (; u < nu; u += stride) {
-    const Unit U = unit_of(G, u);
+  for (; ua < nall; ua += stride) {
+    const uint32_t f = div_magic(ua, G.umag);
+    const Unit U = unit_of(G, ua - f * G.ucum[3]);
     const uint32_t local = U.local0 + b;
     const bool live = local < U.nb;
-    const uint32_t g = U.cum + local;
+    const uint32_t g = f * G.cum[3] + U.cum + local;
     const uint32_t n0 = 16u * q;
     // ---- this unit's rows 2q, 2q+1 into the block's image; the next unit's
     // rows in flight behind this unit's arithmetic
@@ -269,9 +276,9 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
     // in-order vmcnt accounting exact, so the loop top waits for these two
     // loads only, not for the stores behind them)
 #if MYYUV_EXP == 2  // diagnostic: compute only (pixels synthesised, stores below elided)
-    nx = make_uint4(u * 2654435761u + lane, u ^ 0x5bd1e995u, (u + lane) * 40503u, u * 69069u);
+    nx = make_uint4(ua * 2654435761u + lane, ua ^ 0x5bd1e995u, (ua + lane) * 40503u, ua * 69069u);
 #else
-    nx = load_rows(frame, G, u + stride < nu ? u + stride : u, b, q);
+    nx = load_rows(frame, G, ua + stride < nall ? ua + stride : ua, b, q);
 #endif
     wave_sync();
 
@@ -383,21 +390,22 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
   const uint32_t q = lane & 3u, b = lane >> 2;
   float* tb = tile[threadIdx.x >> 6] + b * kTile;
   uint32_t* tw = reinterpret_cast<uint32_t*>(tb);  // the block's int16 image (aliases tb)
-  const uint32_t nu = G.ucum[3], stride = unit_stride();
-  uint32_t u = first_unit();
+  const uint32_t nall = G.ucum[3] * G.nframes, stride = unit_stride();
+  uint32_t ua = first_unit();
   uint4 na = make_uint4(0, 0, 0, 0), nc = na;
-  if (u < nu) load_quads(coef, G, u, b, q, na, nc);
+  if (ua < nall) load_quads(coef, G, ua, b, q, na, nc);
   sink[lane] = make_uint4(0, 0, 0, 0);  // see K1
   sink[64 + lane] = make_uint4(0, 0, 0, 0);
 
-  for (; u < nu; u += stride) {
-    const Unit U = unit_of(G, u);
+  for (; ua < nall; ua += stride) {
+    const uint32_t f = div_magic(ua, G.umag);
+    const Unit U = unit_of(G, ua - f * G.ucum[3]);
     const uint32_t local = U.local0 + b;
     // ---- rows 2q, 2q+1 of coefficients into the block's image (first 32
     // dwords of its tile); the next unit's quads in flight
     *reinterpret_cast<uint4*>(tw + 8 * q) = na;
     *reinterpret_cast<uint4*>(tw + 8 * q + 4) = nc;
-    load_quads(coef, G, u + stride < nu ? u + stride : u, b, q, na, nc);  // unconditional: see K1
+    load_quads(coef, G, ua + stride < nall ? ua + stride : ua, b, q, na, nc);  // unconditional: see K1
     wave_sync();
     // (Z[k][2q], Z[k][2q+1]) = word k*4 + q
     uint32_t zc[8];
@@ -479,8 +487,9 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
     {
       const bool live = local < U.nb;
       const uint32_t off = block_row_offset(U, live ? local : 0u, 2u * q);
-      uint2* d0 = live ? reinterpret_cast<uint2*>(frame + off) : reinterpret_cast<uint2*>(sink + lane);
-      uint2* d1 = live ? reinterpret_cast<uint2*>(frame + off + U.pw)
+      uint8_t* fr = frame + (size_t)f * G.fbytes;
+      uint2* d0 = live ? reinterpret_cast<uint2*>(fr + off) : reinterpret_cast<uint2*>(sink + lane);
+      uint2* d1 = live ? reinterpret_cast<uint2*>(fr + off + U.pw)
                        : reinterpret_cast<uint2*>(sink + 64 + lane);
       *d0 = w0;
       *d1 = w1;

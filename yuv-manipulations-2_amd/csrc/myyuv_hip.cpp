@@ -30,7 +30,7 @@ __global__ void k_huff_encode_wave(const uint4*, uint32_t*, uint8_t*, const uint
                                    const uint32_t*);
 __global__ void k_huff_encode_wide(const uint4*, uint32_t*, uint8_t*,
                                    const uint32_t*, const uint32_t*);
-__global__ void k_scan_chain(const uint8_t*, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
+__global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
                              StreamDesc*, uint32_t*, uint32_t*, uint32_t, unsigned long long*,
                              uint32_t, unsigned long long*);
 __global__ void k_compact(const uint32_t*, const uint8_t*, const uint32_t*, const uint32_t*,
@@ -105,7 +105,7 @@ uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 // (`resident`, from the occupancy query at context creation), never more
 // waves than units.
 dim3 xf_grid(const FrameGeom& G, uint32_t resident) {
-  const uint32_t wgs = ceil_div(G.ucum[3], 4);
+  const uint32_t wgs = ceil_div(G.ucum[3] * G.nframes, 4);
   return dim3(wgs < resident ? wgs : resident);
 }
 
@@ -135,6 +135,19 @@ int make_geom(uint32_t w, uint32_t h, FrameGeom& G) {
   G.poff[0] = 0;
   G.poff[1] = w * h;
   G.poff[2] = w * h + (w / 2) * (h / 2);
+  G.nframes = 1;
+  G.fbytes = w * h / 2 * 3;
+  G.umag = block_magic(G.ucum[3]);
+  return 0;
+}
+
+// A batch of nf frames of G's geometry (block, unit and byte counts of the
+// whole batch must fit 32 bits).
+int set_batch(FrameGeom& G, uint32_t nf) {
+  if (nf == 0) return MYYUV_E_ARG;
+  if ((uint64_t)G.cum[3] * nf > 0xFFFFFFFFull - 4096 || (uint64_t)G.fbytes * nf > 0xFFFFFFFFull)
+    return MYYUV_E_ARG;
+  G.nframes = nf;
   return 0;
 }
 
@@ -247,22 +260,25 @@ int set_qtables(myyuv_hip_ctx* c, const uint8_t q[3], hipStream_t s) {
   return 0;
 }
 
+// Workspace for a batch of G.nframes frames (blocks numbered batch-globally;
+// scan tiles, stream descriptors and look-back status words per frame).
 int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
-  const uint32_t nblk = G.cum[3];
+  const uint32_t nf = G.nframes;
+  const uint32_t nblk = G.cum[3] * nf;
   const uint32_t nwaves = ceil_div(nblk, kWave);
-  const uint32_t ntiles = ceil_div(nblk, kScanTile);
+  const uint32_t ntiles = ceil_div(G.cum[3], kScanTile);
   int e = 0;
   e |= c->coef.grow((size_t)nwaves * kCoefQuadsPerWave * 16);  // natural-order quads
   e |= c->slots.grow((size_t)nwaves * kSlotWords * kWave * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
   e |= c->loff.grow((size_t)nblk * 4);
-  e |= c->tiles.grow((size_t)(ntiles + 1) * 4);
+  e |= c->tiles.grow((size_t)nf * (ntiles + 1) * 4);
   e |= c->err.grow(8);
   e |= c->sink.grow(128 * 16);
   e |= c->psize.grow(4);
-  e |= c->desc.grow(sizeof(StreamDesc));
+  e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
   e |= c->work.grow((size_t)nblk * 4 + 256);  // [0]: overflow count, then block ids
-  const size_t st_bytes = (size_t)(ntiles + 1) * 8;
+  const size_t st_bytes = (size_t)nf * (ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
     // zeroed before any kernel on any stream reads it
@@ -298,8 +314,11 @@ int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, hipStream_t s) {
   return e;
 }
 
+// One batch of G.nframes frames (frame f at d_in + f * fbytes), payload f at
+// d_out + f * cap, its size at d_size[f].
 int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void* d_out,
                     uint32_t cap, uint32_t* d_size, hipStream_t s) {
+  const uint32_t nf = G.nframes;
   const uint32_t nblk = G.cum[3];
   const uint32_t ntiles = ceil_div(nblk, kScanTile);
   const QTables* qt = c->qtd.as<const QTables>();
@@ -308,24 +327,28 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
               static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->sink.as<uint4>(),
               c->work.as<uint32_t>());
-  e |= launch_huff_encode(c, nblk, s);
+  e |= launch_huff_encode(c, nblk * nf, s);
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
   for (int p = 0; p < 3; p++) S.pos[p] = G.cum[p];
-  e |= launch(c, MYYUV_K_SCAN, k_scan_chain, dim3(ntiles), dim3(256), s, c->sizes.as<const uint8_t>(),
-              S, (const uint32_t*)nullptr, 0u, G, (StreamDesc*)nullptr, c->loff.as<uint32_t>(),
-              c->tiles.as<uint32_t>(), ntiles, c->status.as<unsigned long long>(), next_epoch(c), err);
+  e |= launch(c, MYYUV_K_SCAN, k_scan_chain, dim3(ntiles, nf), dim3(256), s,
+              c->sizes.as<const uint8_t>(), nblk, S, (const uint32_t*)nullptr, 0u, G,
+              (StreamDesc*)nullptr, c->loff.as<uint32_t>(), c->tiles.as<uint32_t>(), ntiles,
+              c->status.as<unsigned long long>(), next_epoch(c), err);
   const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], 256), t1 = ceil_div(G.cum[2] - G.cum[1], 256),
                  t2 = ceil_div(G.cum[3] - G.cum[2], 256);
-  e |= launch(c, MYYUV_K_COMPACT, k_compact, dim3(t0 + t1 + t2), dim3(256), s,
+  e |= launch(c, MYYUV_K_COMPACT, k_compact, dim3(t0 + t1 + t2, nf), dim3(256), s,
               c->slots.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
               c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
               static_cast<uint8_t*>(d_out), cap, d_size, err);
   return e ? MYYUV_E_HIP : 0;
 }
 
+// The mirror: payload f at d_in + f * cap (size d_size[f]) -> frame f at
+// d_out + f * fbytes.
 int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
                       const uint32_t* d_size, uint32_t cap, void* d_out, hipStream_t s) {
+  const uint32_t nf = G.nframes;
   const uint32_t nblk = G.cum[3];
   const uint32_t ntiles = ceil_div(nblk, kScanTile);
   const QTables* qt = c->qtd.as<const QTables>();
@@ -336,13 +359,13 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
   for (int p = 0; p < 3; p++) S.pos[p] = 0;
-  e |= launch(c, MYYUV_K_SCAN, k_scan_chain, dim3(ntiles), dim3(256), s, in, S, d_size, cap, G, desc,
-              c->loff.as<uint32_t>(), c->tiles.as<uint32_t>(), ntiles,
+  e |= launch(c, MYYUV_K_SCAN, k_scan_chain, dim3(ntiles, nf), dim3(256), s, in, cap, S, d_size, cap,
+              G, desc, c->loff.as<uint32_t>(), c->tiles.as<uint32_t>(), ntiles,
               c->status.as<unsigned long long>(), next_epoch(c), err);
   const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], kWave),
                  t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
-  e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2), dim3(kWave), s, in, d_size,
+  e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size,
               cap, (const StreamDesc*)desc, c->loff.as<const uint32_t>(),
               c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<uint4>(), err);
   e |= launch(c, MYYUV_K_IDCT, k_dequant_idct, xf_grid(G, c->xf_resident[1]), dim3(256), s,
@@ -484,38 +507,62 @@ int myyuv_hip_reserve(myyuv_hip_handle c, uint32_t w, uint32_t h) {
   return reserve(c, G);
 }
 
-int myyuv_gpu_dct_compress_device(myyuv_hip_handle c, const void* d_in, uint32_t w, uint32_t h,
-                                  const uint8_t q[3], void* d_out, uint32_t cap,
-                                  uint32_t* d_size, void* stream) {
-  if (!c || !d_in || !d_out || !d_size || !q) return MYYUV_E_ARG;
-  if (((uintptr_t)d_out & 3) || ((uintptr_t)d_in & 7)) return MYYUV_E_ARG;
+int myyuv_gpu_dct_compress_batch_device(myyuv_hip_handle c, const void* d_in, uint32_t nframes,
+                                        uint32_t w, uint32_t h, const uint8_t q[3], void* d_out,
+                                        uint32_t cap, uint32_t* d_sizes, void* stream) {
+  if (!c || !d_in || !d_out || !d_sizes || !q) return MYYUV_E_ARG;
+  if (((uintptr_t)d_out & 3) || ((uintptr_t)d_in & 7) || (nframes > 1 && (cap & 3)))
+    return MYYUV_E_ARG;
   for (int p = 0; p < 3; p++)
     if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
   FrameGeom G;
   int e = make_geom(w, h, G);
-  if (e) return e;
+  if (e || (e = set_batch(G, nframes))) return e;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
   if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
-  return launch_compress(c, G, d_in, d_out, cap, d_size, s);
+  return launch_compress(c, G, d_in, d_out, cap, d_sizes, s);
+}
+
+int myyuv_gpu_dct_decompress_batch_device(myyuv_hip_handle c, const void* d_in, const uint32_t* d_sizes,
+                                          uint32_t cap, uint32_t nframes, uint32_t w, uint32_t h,
+                                          const uint8_t q[3], void* d_out, void* stream) {
+  if (!c || !d_in || !d_out || !d_sizes || !q) return MYYUV_E_ARG;
+  if (((uintptr_t)d_in & 3) || ((uintptr_t)d_out & 7) || (nframes > 1 && (cap & 3)))
+    return MYYUV_E_ARG;
+  for (int p = 0; p < 3; p++)
+    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e || (e = set_batch(G, nframes))) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
+  return launch_decompress(c, G, d_in, d_sizes, cap, d_out, s);
+}
+
+int myyuv_gpu_dct_compress_device(myyuv_hip_handle c, const void* d_in, uint32_t w, uint32_t h,
+                                  const uint8_t q[3], void* d_out, uint32_t cap,
+                                  uint32_t* d_size, void* stream) {
+  return myyuv_gpu_dct_compress_batch_device(c, d_in, 1, w, h, q, d_out, cap, d_size, stream);
 }
 
 int myyuv_gpu_dct_decompress_device(myyuv_hip_handle c, const void* d_in, const uint32_t* d_size,
                                     uint32_t cap, uint32_t w, uint32_t h, const uint8_t q[3],
                                     void* d_out, void* stream) {
-  if (!c || !d_in || !d_out || !d_size || !q) return MYYUV_E_ARG;
-  if (((uintptr_t)d_in & 3) || ((uintptr_t)d_out & 7)) return MYYUV_E_ARG;
-  for (int p = 0; p < 3; p++)
-    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  return myyuv_gpu_dct_decompress_batch_device(c, d_in, d_size, cap, 1, w, h, q, d_out, stream);
+}
+
+int myyuv_hip_reserve_batch(myyuv_hip_handle c, uint32_t w, uint32_t h, uint32_t nframes) {
+  if (!c) return MYYUV_E_ARG;
   FrameGeom G;
   int e = make_geom(w, h, G);
-  if (e) return e;
+  if (e || (e = set_batch(G, nframes))) return e;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
-  return launch_decompress(c, G, d_in, d_size, cap, d_out, s);
+  return reserve(c, G);
 }
 
 int myyuv_hip_sync_status(myyuv_hip_handle c, void* stream, int64_t* bad_block) {
@@ -711,6 +758,9 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
   G.bmag[0] = block_magic(1);
   G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
   G.ucum[1] = G.ucum[2] = G.ucum[3] = ceil_div(nblocks, kXfUnit);
+  G.nframes = 1;
+  G.fbytes = nblocks * 64;
+  G.umag = block_magic(G.ucum[3]);
   QTables t;
   std::memset(&t, 0, sizeof(t));
   std::memcpy(t.q[0], qtable, 256);
@@ -753,6 +803,7 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   FrameGeom G;
   std::memset(&G, 0, sizeof(G));
   G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
+  G.nframes = 1;
   if (reserve(c, G)) return MYYUV_E_HIP;
   const uint32_t nwaves = ceil_div(nblocks, kWave);
   // host-side relayout into K1's output format: natural-order quads

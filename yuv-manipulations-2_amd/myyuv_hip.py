@@ -29,7 +29,8 @@ EXPORTS = [
     "myyuv_gpu_dct_compress", "myyuv_gpu_dct_decompress", "myyuv_hip_reserve",
     "myyuv_gpu_dct_compress_device", "myyuv_gpu_dct_decompress_device", "myyuv_hip_sync_status",
     "myyuv_hip_profile", "myyuv_hip_profile_kernels", "myyuv_hip_kernel_stats", "myyuv_gpu_fdct_blocks",
-    "myyuv_gpu_huff_encode_blocks",
+    "myyuv_gpu_huff_encode_blocks", "myyuv_hip_reserve_batch", "myyuv_gpu_dct_compress_batch_device",
+    "myyuv_gpu_dct_decompress_batch_device",
 ]
 
 _lib = None
@@ -83,6 +84,9 @@ def load():
     L.myyuv_hip_reserve.argtypes = [vp, u32, u32]
     L.myyuv_gpu_dct_compress_device.argtypes = [vp, vp, u32, u32, u8p, vp, u32, vp, vp]
     L.myyuv_gpu_dct_decompress_device.argtypes = [vp, vp, vp, u32, u32, u32, u8p, vp, vp]
+    L.myyuv_hip_reserve_batch.argtypes = [vp, u32, u32, u32]
+    L.myyuv_gpu_dct_compress_batch_device.argtypes = [vp, vp, u32, u32, u32, u8p, vp, u32, vp, vp]
+    L.myyuv_gpu_dct_decompress_batch_device.argtypes = [vp, vp, vp, u32, u32, u32, u32, u8p, vp, vp]
     L.myyuv_hip_sync_status.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int64)]
     L.myyuv_hip_profile.argtypes = [vp, ctypes.c_int]
     L.myyuv_hip_profile_kernels.argtypes = [vp, ctypes.c_uint32]
@@ -176,6 +180,25 @@ class Codec:
     def decompress_device(self, d_payload, d_size, cap, w, h, q, d_iyuv, stream=None):
         rc = load().myyuv_gpu_dct_decompress_device(self._h, d_payload, d_size, cap, w, h,
                                                     _u8(_q(q)), d_iyuv, stream)
+        if rc:
+            raise CodecError(rc)
+
+    # batches: frame f at d_iyuv + f*W*H*3/2, payload f at d_payload + f*cap,
+    # its size at d_sizes[f] (u32)
+    def reserve_batch(self, w, h, nframes):
+        rc = load().myyuv_hip_reserve_batch(self._h, w, h, nframes)
+        if rc:
+            raise CodecError(rc)
+
+    def compress_batch_device(self, d_iyuv, nframes, w, h, q, d_payload, cap, d_sizes, stream=None):
+        rc = load().myyuv_gpu_dct_compress_batch_device(self._h, d_iyuv, nframes, w, h, _u8(_q(q)),
+                                                        d_payload, cap, d_sizes, stream)
+        if rc:
+            raise CodecError(rc)
+
+    def decompress_batch_device(self, d_payload, d_sizes, cap, nframes, w, h, q, d_iyuv, stream=None):
+        rc = load().myyuv_gpu_dct_decompress_batch_device(self._h, d_payload, d_sizes, cap, nframes, w,
+                                                          h, _u8(_q(q)), d_iyuv, stream)
         if rc:
             raise CodecError(rc)
 
