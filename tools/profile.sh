@@ -12,9 +12,9 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-  python3 $R/bench.py --steps $STEPS --warmup 3 --cpu-seconds 0 > $OUT/bench_trace.json 2> $OUT/bench_trace.err
+  python3 $R/bench.py --steps $STEPS --warmup 3 --cpu-seconds 0 --breakdown-steps 0 > $OUT/bench_trace.json 2> $OUT/bench_trace.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- \
-  python3 $R/bench.py --steps $STEPS --warmup 3 --cpu-seconds 0 --no-kernel-events > $OUT/bench_fetch.json 2> $OUT/bench_fetch.err
+  python3 $R/bench.py --steps $STEPS --warmup 3 --cpu-seconds 0 --breakdown-steps 0 --no-kernel-events > $OUT/bench_fetch.json 2> $OUT/bench_fetch.err
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- \
-  python3 $R/bench.py --steps $STEPS --warmup 3 --cpu-seconds 0 --no-kernel-events > $OUT/bench_write.json 2> $OUT/bench_write.err
+  python3 $R/bench.py --steps $STEPS --warmup 3 --cpu-seconds 0 --breakdown-steps 0 --no-kernel-events > $OUT/bench_write.json 2> $OUT/bench_write.err
 echo done > $OUT/DONE
