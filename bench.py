@@ -59,8 +59,8 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=240)
+    ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--quality", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the cpu_baseline sample (0 disables it)")

@@ -105,7 +105,8 @@ constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
 #define MYYUV_WAVE_LIMIT 24576
 #endif
 constexpr uint32_t kWaveEncodeLimit = MYYUV_WAVE_LIMIT;
-constexpr uint32_t kWaveEncodeGrid = 16384;  // waves of k_huff_encode_wave
+constexpr uint32_t kWaveEncodeGrid = 8192;   // waves of k_huff_encode_wave (grid-stride)
+constexpr uint32_t kWideGrid = 1280;         // workgroups of k_huff_encode_wide: 5 per CU fit its LDS
 #ifndef MYYUV_K2_GROUP
 #define MYYUV_K2_GROUP 256
 #endif

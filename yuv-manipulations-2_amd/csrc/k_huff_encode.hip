@@ -721,10 +721,11 @@ __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict
                                                         uint32_t* __restrict__ slots,
                                                         uint8_t* __restrict__ sizes,
                                                         const uint32_t* __restrict__ work,
-                                                        const uint32_t* __restrict__ work_count) {
+                                                        const uint32_t* __restrict__ work_count,
+                                                        uint32_t limit) {
   __shared__ uint32_t img[kSlotWords + 2];
   const uint32_t cnt = *work_count;
-  if (cnt > kWaveEncodeLimit) return;
+  if (cnt > limit) return;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) encode_block_wave(coef, work[i], img, slots, sizes, i);
 }
 
@@ -827,27 +828,33 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
 // Overflow pass (CAP=64), lane per block, for long worklists (noise-like
 // frames where most blocks overflow): the blocks listed in `work` (count in
 // *work_count), 64 per workgroup; the grid is sized for the worst case, idle
-// groups exit.  Short lists go to k_huff_encode_wave instead.
+// groups exit.  Lists of at most `limit` blocks go to k_huff_encode_wave instead.
 __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict__ coef,
                                                         uint32_t* __restrict__ slots,
                                                         uint8_t* __restrict__ sizes,
                                                         const uint32_t* __restrict__ work,
-                                                        const uint32_t* __restrict__ work_count) {
+                                                        const uint32_t* __restrict__ work_count,
+                                                        uint32_t limit) {
   constexpr int CAP = 64;
   __shared__ uint32_t lds[Layout<CAP>::kWords * kWave];
   const uint32_t cnt = *work_count;
-  const uint32_t i = blockIdx.x * kWave + threadIdx.x;
-  if (cnt <= kWaveEncodeLimit || blockIdx.x * kWave >= cnt) return;  // small lists: k_huff_encode_wave
-  const bool live = i < cnt;
-  const uint32_t g = live ? work[i] : 0;
-  CoefRegs R;
-  R.load(coef, g);
-  const int msz = live ? R.msz() : 0;
-  const int wmsz = wave_max(msz);
-  if (!live) return;
-  const Img<CAP> I{lds, (int)threadIdx.x};
-  encode_block<CAP>(I, R, msz, max(wmsz, 1),
-                    slots + (size_t)(g >> 6) * (kSlotWords * kWave) + (g & 63), sizes + g);
+  if (cnt <= limit) return;  // short lists: k_huff_encode_wave
+  // grid-stride over 64-block slices of the list (the grid is what the
+  // 32 KB-per-workgroup LDS lets be resident)
+  for (uint32_t base = blockIdx.x * kWave; base < cnt; base += gridDim.x * kWave) {
+    const uint32_t i = base + threadIdx.x;
+    const bool live = i < cnt;
+    const uint32_t g = live ? work[i] : 0;
+    CoefRegs R;
+    R.load(coef, g);
+    const int msz = live ? R.msz() : 0;
+    const int wmsz = wave_max(msz);
+    if (live) {
+      const Img<CAP> I{lds, (int)threadIdx.x};
+      encode_block<CAP>(I, R, msz, max(wmsz, 1),
+                        slots + (size_t)(g >> 6) * (kSlotWords * kWave) + (g & 63), sizes + g);
+    }
+  }
 }
 
 }  // namespace myyuv_gpu

@@ -27,9 +27,9 @@ __global__ void k_dequant_idct(const uint4*, FrameGeom, const QTables*, uint8_t*
 __global__ void k_huff_encode(const uint4*, uint32_t, uint32_t*, uint8_t*,
                               uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, uint32_t*, uint8_t*, const uint32_t*,
-                                   const uint32_t*);
+                                   const uint32_t*, uint32_t);
 __global__ void k_huff_encode_wide(const uint4*, uint32_t*, uint8_t*,
-                                   const uint32_t*, const uint32_t*);
+                                   const uint32_t*, const uint32_t*, uint32_t);
 __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
                              StreamDesc*, uint32_t*, uint32_t*, uint32_t, unsigned long long*,
                              uint32_t, unsigned long long*);
@@ -171,6 +171,7 @@ struct myyuv_hip_ctx {
   bool q_valid = false;
   // profiling
   uint32_t prof = 0;  // bit k: stamp kernel id k
+  uint32_t skip = 0;  // diagnostic: bit k: do not launch kernel id k (myyuv_debug_skip_kernels)
   double ms[MYYUV_K_COUNT] = {};
   int64_t launches[MYYUV_K_COUNT] = {};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -210,6 +211,7 @@ hipEvent_t take_event(myyuv_hip_ctx* c) {
 template <class... KArgs, class... Args>
 int launch(myyuv_hip_ctx* c, int kid, void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t s,
            Args... args) {
+  if ((c->skip >> kid) & 1u) return 0;
   hipEvent_t a = nullptr, b = nullptr;
   const bool stamp = (c->prof >> kid) & 1u;
   if (stamp) {
@@ -296,21 +298,27 @@ uint32_t next_epoch(myyuv_hip_ctx* c) {
 
 // K2: fast pass over all blocks, then the overflow pass over the blocks with
 // more than 8 distinct symbols (worklist filled on the device; no host sync):
-// wave-per-block for short lists, lane-per-block for long ones — both
-// kernels are queued and each returns at once outside its regime.
-int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, hipStream_t s) {
+// wave-per-block for lists of at most kWaveEncodeLimit blocks, lane-per-block
+// for longer ones; both kernels are queued and each returns at once outside
+// its regime.  A batch (nf > 1) takes the lane-per-block pass only: its list
+// is long, and the wave pass's per-block SALU cost would crowd the other
+// launch groups in flight (tools/kskip.py).
+int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, uint32_t nf, hipStream_t s) {
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
+  const uint32_t limit = nf > 1 ? 0u : kWaveEncodeLimit;
   int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(ceil_div(nblk, kK2Group)), dim3(kK2Group), s,
                  c->coef.as<const uint4>(), nblk, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
                  list, count);
-  e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
+  if (limit > 0)
+    e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
+                c->coef.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
+                (const uint32_t*)list, (const uint32_t*)count, limit);
+  const uint32_t wide = ceil_div(nblk, kWave) < kWideGrid ? ceil_div(nblk, kWave) : kWideGrid;
+  e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(wide), dim3(kWave), s,
               c->coef.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
-              (const uint32_t*)list, (const uint32_t*)count);
-  e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(ceil_div(nblk, kWave)), dim3(kWave), s,
-              c->coef.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
-              (const uint32_t*)list, (const uint32_t*)count);
+              (const uint32_t*)list, (const uint32_t*)count, limit);
   return e;
 }
 
@@ -327,7 +335,9 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
               static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->sink.as<uint4>(),
               c->work.as<uint32_t>());
-  e |= launch_huff_encode(c, nblk * nf, s);
+  if ((c->skip >> MYYUV_K_FDCT) & 1u)  // diagnostic skip: keep K1's reset of the overflow count
+    e |= hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess;
+  e |= launch_huff_encode(c, nblk * nf, nf, s);
   ScanSrc S;
   for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
   for (int p = 0; p < 3; p++) S.pos[p] = G.cum[p];
@@ -710,6 +720,16 @@ int myyuv_debug_k2_wstamps(uint32_t* out, uint32_t n) {
 #endif
 }
 
+// Diagnostic: stop launching the kernels whose bit (1 << MYYUV_K_*) is set,
+// to measure each kernel's share of a pipelined run.  The buffers keep what the
+// last real launch wrote, so repeating identical frames still decodes.
+int myyuv_debug_skip_kernels(myyuv_hip_handle c, uint32_t mask) {
+  if (!c) return MYYUV_E_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->skip = mask;
+  return 0;
+}
+
 // Diagnostic builds (-DMYYUV_STAMPS): summed per-stage wave cycles of K2
 // since the last call; returns MYYUV_E_ARG in normal builds.
 int myyuv_debug_k2_stamps(unsigned long long out[40]) {
@@ -817,7 +837,7 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess)  // K1 zeroes it in the codec path
     return MYYUV_E_HIP;
-  if (launch_huff_encode(c, nblocks, s)) return MYYUV_E_HIP;
+  if (launch_huff_encode(c, nblocks, 1, s)) return MYYUV_E_HIP;
   std::vector<uint32_t> slots((size_t)nwaves * kSlotWords * kWave);
   if (hipMemcpyAsync(slots.data(), c->slots.p, slots.size() * 4, hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
