@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4,
                     help="frames per launch (the batch entry points): each kernel covers this "
                          "many frames")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the side measurements (decode-only rate, K7 BMP->IYUV roofline)")
     ap.add_argument("--breakdown-steps", type=int, default=5,
                     help="untimed steps after the timed region with every kernel stamped")
     return ap.parse_args()
@@ -256,6 +258,54 @@ def main():
         codec.sync_status(sps[0])
         breakdown = codec.kernel_stats()
         codec.profile(False)
+    # side measurements, outside the timed region
+    side = None
+    if rank == 0 and not args.no_side:
+        side = {}
+        # decode-only batched rate: the same launch groups, decompress only,
+        # from the streams the timed region left in HBM
+        full = max(1, args.steps // B)  # groups whose B slots all hold a stream
+
+        def dgroup(j):
+            k = j % nf
+            f0 = (j % full) * B
+            codecs[k].decompress_batch_device(d_pay[f0].data_ptr(), d_size[f0:f0 + B].data_ptr(), cap, B,
+                                              w, h, (q, q, q), d_out[k].data_ptr(), sps[k])
+        nd = max(nf, args.steps // B)
+        for j in range(nf):
+            dgroup(j)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for j in range(nd):
+            dgroup(j)
+        for st in streams[1:]:
+            streams[0].wait_stream(st)
+        torch.cuda.synchronize(dev)
+        td = time.perf_counter() - t0
+        check_status()
+        side["decode_only"] = {"value": round(nd * B * mp / td, 2), "unit": "MP/s", "frames": nd * B}
+        # K7 BMP -> IYUV on a 4032x3008 BGRA bottom-up frame: 4 B in + 1.5 B out
+        # per pixel, streaming, so its bound is HBM
+        bgra = torch.randint(0, 256, (w * h * 4,), dtype=torch.uint8, device=dev)
+        d_iy = torch.empty(w * h * 3 // 2, dtype=torch.uint8, device=dev)
+        sp0 = sps[0]
+        for _ in range(3):
+            codec.bmp_to_iyuv_device(bgra.data_ptr(), w, h, 32, d_iy.data_ptr(), sp0)
+        codec.sync_status(sp0)
+        codec.profile(True, kernels=["bmp_to_iyuv"])
+        for _ in range(50):
+            codec.bmp_to_iyuv_device(bgra.data_ptr(), w, h, 32, d_iy.data_ptr(), sp0)
+        codec.sync_status(sp0)
+        kms, kn = codec.kernel_stats()["bmp_to_iyuv"]
+        codec.profile(False)
+        if kn:
+            alg = w * h * 4 + w * h * 3 // 2
+            a7 = alg / (kms / kn * 1e-3) / 1e9
+            side["bmp_to_iyuv"] = {"bound": "hbm", "achieved": round(a7, 1), "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": round(a7 / HBM_PEAK_GBS, 4),
+                                   "algorithmic_bytes_per_launch": alg,
+                                   "avg_launch_us": round(kms / kn * 1e3, 2), "frame": f"{w}x{h} BGRA"}
+        del bgra, d_iy
     if world > 1:
         tt = torch.tensor([t], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -302,6 +352,7 @@ def main():
                        "launch_groups_in_flight": nf, "frames_per_launch": B, "payload_bytes": n0},
             "roofline": roof, "roofline_isolated": roof_iso, "cpu_baseline": cpu,
             "kernel_us": kernel_us or None,
+            "side": side,
         }
         print(json.dumps(line), flush=True)
     for c in codecs:

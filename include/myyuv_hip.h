@@ -48,6 +48,9 @@ extern "C" {
 #define MYYUV_E_BAD_CHUNK 12      /* malformed chunk header/table (reference: assert / UB) */
 #define MYYUV_E_HIP 13            /* HIP runtime failure */
 #define MYYUV_E_NO_DEVICE 14      /* no gfx950 device / HIP unavailable */
+#define MYYUV_E_BMP_INVALID 15    /* myyuv_yuv.cpp:514 "BMP is invalid" (width % 4, bit_count 0) */
+#define MYYUV_E_BMP_SIGN 16       /* myyuv_bmp.cpp:98 "Unaccounted width and height sign" */
+#define MYYUV_E_BMP_UNSUPPORTED 17 /* odd height or not 24/32 bpp (reference: assert, myyuv_yuv.cpp:92,97) */
 
 typedef struct myyuv_hip_ctx* myyuv_hip_handle;
 
@@ -116,6 +119,21 @@ int myyuv_gpu_dct_decompress_batch_device(myyuv_hip_handle h, const void* d_payl
                                           const uint32_t* d_payload_sizes, uint32_t cap,
                                           uint32_t nframes, uint32_t width, uint32_t height,
                                           const uint8_t quality[3], void* d_iyuv, void* stream);
+/* BMP -> IYUV: replaces YUV(const BMP&, IYUV), i.e.
+ * YUV::bmp_to_yuv_map[IYUV] (myyuv_yuv.cpp:88-128) over BMP::colorData
+ * (myyuv_bmp.cpp:77-101).  `bmp_data` is BMP::data — the pixel array as stored
+ * in the file (BGR or BGRA, bit_count 24 or 32, |width| % 4 == 0 so rows are
+ * unpadded); `width` / `height` are the header's signed fields, whose signs
+ * select colorData's orientation (height > 0: bottom-up rows; width < 0:
+ * pixel order reversed).  Writes |width|*|height|*3/2 IYUV bytes.  The C++
+ * adapter checks the rest of BMP::isValidHeader and writes the YUV header. */
+int myyuv_gpu_bmp_to_iyuv(myyuv_hip_handle h, const uint8_t* bmp_data, int32_t width,
+                          int32_t height, uint16_t bit_count, uint8_t* iyuv);
+/* Device-resident variant, asynchronous on `stream` (NULL = the context's);
+ * argument errors are returned at once. */
+int myyuv_gpu_bmp_to_iyuv_device(myyuv_hip_handle h, const void* d_bmp_data, int32_t width,
+                                 int32_t height, uint16_t bit_count, void* d_iyuv, void* stream);
+
 /* Waits for `stream`, returns (and clears) the first device-side error since
  * the last call; *bad_block as above. */
 int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
@@ -135,7 +153,8 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
 #define MYYUV_K_HUFF_WIDE 7  /* K2 overflow pass, lane per block (long worklists) */
 #define MYYUV_K_SCAN_SUMS 8  /* (unused: the scan is single-pass) */
 #define MYYUV_K_HUFF_WAVE 9  /* K2 overflow pass, wave per block (short worklists) */
-#define MYYUV_K_COUNT 10
+#define MYYUV_K_BMP 10       /* K7 bmp_to_iyuv (BMP -> IYUV conversion) */
+#define MYYUV_K_COUNT 11
 int myyuv_hip_profile(myyuv_hip_handle h, int enable);
 /* As myyuv_hip_profile, but stamps only the kernels whose bit (1 << MYYUV_K_*)
  * is set in `mask` (0 disables): event stamping costs host and queue time per

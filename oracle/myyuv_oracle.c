@@ -732,3 +732,67 @@ void oracle_set_num_threads(int n) {
     (void)n;
 #endif
 }
+
+/* ------------------------------------------------------------------------
+ * BMP -> IYUV: YUV(const BMP&, IYUV), i.e.
+ * bmp_to_yuv_map[IYUV] (myyuv_yuv.cpp:88-128) over BMP::colorData
+ * (myyuv_bmp.cpp:77-101), with getYUV444FromRGB2x2 (myyuv_yuv.cpp:34-52) and
+ * divide_roundnearest<uint8_t> (:20-27).
+ *
+ * bmp_data is BMP::data (the pixel array as stored in the file: BGR(A),
+ * `bit_count` bits per pixel, no row padding since width % 4 == 0).
+ * colorData's orientation: width > 0, height < 0 -> as stored; width < 0,
+ * height > 0 -> pixel order reversed; both > 0 -> rows bottom-up.
+ * Numerics as the reference's x86-64 -O3 build: fp32 products and sums left
+ * to right, no contraction; float -> uint8_t casts truncate toward zero
+ * through a 32-bit integer and keep the low byte (cvttss2si); the 4-term
+ * chroma sum wraps mod 256 (a saturated-blue quad has Cb 0).
+ * ---------------------------------------------------------------------- */
+static uint8_t bmp_cast_u8(float x) { return (uint8_t)(int32_t)x; }
+
+static void bmp_yuv444(const uint8_t* px, uint8_t* y, uint8_t* cb, uint8_t* cr) {
+  const float B = (float)px[0], G = (float)px[1], R = (float)px[2];
+  const float Y = 0.299f * R + 0.587f * G + 0.114f * B;
+  *y = bmp_cast_u8(Y);
+  *cb = (uint8_t)(bmp_cast_u8((B - Y) * 0.564f) + 128);
+  *cr = (uint8_t)(bmp_cast_u8((R - Y) * 0.713f) + 128);
+}
+
+int oracle_bmp_to_iyuv(const uint8_t* bmp_data, int32_t width, int32_t height, uint32_t bit_count,
+                       uint8_t* iyuv) {
+  const uint32_t W = (uint32_t)(width < 0 ? -(int64_t)width : width);
+  const uint32_t H = (uint32_t)(height < 0 ? -(int64_t)height : height);
+  if (W % 4 != 0 || bit_count == 0) return ORACLE_E_BMP_INVALID;
+  if (!((width > 0 && height < 0) || (width < 0 && height > 0) || (width > 0 && height > 0)))
+    return ORACLE_E_BMP_SIGN;
+  if ((bit_count != 24 && bit_count != 32) || H % 2 != 0) return ORACLE_E_BMP_UNSUPPORTED;
+  const uint32_t bpp = bit_count / 8;
+  const size_t npx = (size_t)W * H;
+  uint8_t* u = iyuv + npx;
+  uint8_t* v = iyuv + npx + npx / 4;
+  for (uint32_t j = 0; j < H; j += 2)
+    for (uint32_t i = 0; i < W; i += 2) {
+      uint8_t y4[4], cb4[4], cr4[4];
+      for (int q = 0; q < 4; q++) {
+        const uint32_t r = j + (q >> 1), c = i + (q & 1);
+        size_t src;
+        if (width > 0 && height < 0)
+          src = (size_t)r * W + c;
+        else if (width < 0)
+          src = npx - 1 - ((size_t)r * W + c);
+        else
+          src = (size_t)(H - 1 - r) * W + c;
+        bmp_yuv444(bmp_data + src * bpp, &y4[q], &cb4[q], &cr4[q]);
+        iyuv[(size_t)r * W + c] = y4[q];
+      }
+      uint8_t scb = 0, scr = 0;
+      for (int q = 0; q < 4; q++) {
+        scb = (uint8_t)(scb + (uint8_t)((cb4[q] + 2) / 4));
+        scr = (uint8_t)(scr + (uint8_t)((cr4[q] + 2) / 4));
+      }
+      const size_t k = (size_t)(j / 2) * (W / 2) + i / 2;
+      u[k] = scb;
+      v[k] = scr;
+    }
+  return 0;
+}

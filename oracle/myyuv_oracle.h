@@ -26,6 +26,10 @@ extern "C" {
 #define ORACLE_E_UNKNOWN_SYMBOL 11 /* "Huffman unknown symbol" */
 #define ORACLE_E_BAD_CHUNK 12     /* malformed chunk (reference: UB / assert) */
 
+#define ORACLE_E_BMP_INVALID 15    /* "BMP is invalid" */
+#define ORACLE_E_BMP_SIGN 16       /* "Unaccounted width and height sign" */
+#define ORACLE_E_BMP_UNSUPPORTED 17 /* odd dimensions / not 24 or 32 bpp (reference: assert) */
+
 const uint8_t* oracle_zigzag(void);
 const float* oracle_dct_matrix(void);
 void oracle_qtable(int q, int chroma, float out[64]);
@@ -38,6 +42,8 @@ int oracle_compress(const uint8_t* iyuv, uint32_t w, uint32_t h, const uint8_t q
                     uint8_t* payload, uint32_t cap, uint32_t* out_size);
 int oracle_decompress(const uint8_t* payload, uint32_t size, uint32_t w, uint32_t h,
                       const uint8_t q[3], uint8_t* iyuv);
+int oracle_bmp_to_iyuv(const uint8_t* bmp_data, int32_t width, int32_t height, uint32_t bit_count,
+                       uint8_t* iyuv);
 int oracle_num_threads(void);
 void oracle_set_num_threads(int n);
 

@@ -109,3 +109,18 @@ def set_num_threads(n):
 
 def num_threads():
     return lib().oracle_num_threads()
+
+
+def bmp_to_iyuv(bmp_data, width, height, bit_count):
+    """BMP::data (as stored) -> IYUV bytes (myyuv_yuv.cpp:88-128 over
+    myyuv_bmp.cpp:77-101).  Raises RuntimeError(code) as the C ABI does."""
+    src = np.frombuffer(bytes(bmp_data), np.uint8).copy()
+    W, H = abs(width), abs(height)
+    out = np.zeros(max(1, W * H * 3 // 2), np.uint8)
+    L = lib()
+    L.oracle_bmp_to_iyuv.argtypes = [ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint8)]
+    rc = L.oracle_bmp_to_iyuv(_p(src), int(width), int(height), int(bit_count), _p(out))
+    if rc:
+        raise RuntimeError(rc)
+    return out[: W * H * 3 // 2].tobytes()

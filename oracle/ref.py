@@ -79,3 +79,20 @@ def bench(iyuv, w, h, q, iters, variant="omp"):
     if rc:
         raise RefError(L.ref_last_error().decode())
     return tc.value, td.value
+
+
+def bmp_to_iyuv(path, variant="serial"):
+    """myyuv::BMP(path) -> YUV(bmp, IYUV) of the reference (ref_harness.cpp);
+    returns (width, height, iyuv bytes)."""
+    L = lib(variant)
+    L.ref_bmp_to_iyuv.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint32,
+                                  ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    cap = max(1, os.path.getsize(path))  # the IYUV frame is smaller than the BMP file
+    out = np.zeros(cap, np.uint8)
+    w, h = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    rc = L.ref_bmp_to_iyuv(os.fsencode(path), _p(out), cap, ctypes.byref(w), ctypes.byref(h))
+    if rc == 1:
+        raise RefError(L.ref_last_error().decode())
+    if rc:
+        raise RuntimeError(f"ref_bmp_to_iyuv rc={rc}")
+    return w.value, h.value, out[: w.value * h.value * 3 // 2].tobytes()

@@ -116,4 +116,23 @@ int ref_bench(const uint8_t* iyuv, uint32_t w, uint32_t h, const uint8_t q[3], i
   }
 }
 
+// BMP -> IYUV through the reference's public surface: myyuv::BMP(path)
+// (myyuv_bmp.cpp:9-11, 141-166) and YUV(const BMP&, IYUV) (myyuv_yuv.cpp:186-188,
+// 512-523 -> bmp_to_yuv_map, :88-128).  Writes W*H*3/2 bytes (cap checked),
+// the frame size, and the header fields the conversion sets.
+int ref_bmp_to_iyuv(const char* path, uint8_t* out, uint32_t cap, uint32_t* w, uint32_t* h) {
+  try {
+    myyuv::BMP bmp(path);
+    myyuv::YUV y(bmp, myyuv::YUV::FourccFormats::IYUV);
+    *w = y.header.width;
+    *h = y.header.height;
+    if (y.header.data_size > cap) return 2;
+    std::memcpy(out, y.data, y.header.data_size);
+    return 0;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return 1;
+  }
+}
+
 }  // extern "C"

@@ -97,3 +97,39 @@ def test_cli_bad_quality_fails_like_reference(tmp_path):
     r = run(CLI, SMALL, "-compress", "DCT", "0", "-o", str(tmp_path / "x"))
     assert r.returncode != 0
     assert "Compression parameters for DCT must range between [1..100]" in r.stderr
+
+
+def _bmp_file(tmp_path):
+    import gzip
+
+    p = tmp_path / "chef.bmp"
+    p.write_bytes(gzip.open(os.path.join(GOLDEN, "chef-with-trumpet.bmp.gz")).read())
+    return str(p)
+
+
+def test_bmp_info_matches_reference(tmp_path):
+    need_ref()
+    bmp = _bmp_file(tmp_path)
+    a, b = run(CLI, bmp, "-info"), run(REF_CLI, bmp, "-info")
+    assert a.returncode == b.returncode == 0
+    assert a.stdout == b.stdout
+
+
+def test_bmp_argument_errors_match_reference(tmp_path):
+    need_ref()
+    bmp = _bmp_file(tmp_path)
+    for args in ([bmp, "-bogus"], [bmp, "-to_yuv", "IYUV"], [bmp, "-to_yuv", "IYUV", "-x", "o"]):
+        a, b = run(CLI, *args), run(REF_CLI, *args)
+        assert a.returncode == b.returncode, args
+        assert a.stdout.splitlines()[0] == b.stdout.splitlines()[0], args
+
+
+@pytest.mark.gpu
+def test_cli_to_yuv_matches_golden(tmp_path):
+    """myyuv_cli chef.bmp -to_yuv IYUV -o out: the reference's own
+    chef-with-trumpet.myyuv, byte for byte (header included)."""
+    out = tmp_path / "o.myyuv"
+    r = run(CLI, _bmp_file(tmp_path), "-to_yuv", "IYUV", "-o", str(out))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "BMP to YUV (IYUV) : " in r.stdout and r.stdout.endswith("Success!\n")
+    assert out.read_bytes() == open(SMALL, "rb").read()

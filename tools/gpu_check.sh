@@ -1,0 +1,8 @@
+#!/bin/bash
+# GPU parity tests + one default bench line (gpurun: bash tools/gpu_check.sh)
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)} && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH_FAILED; tail -30 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json

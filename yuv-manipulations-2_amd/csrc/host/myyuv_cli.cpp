@@ -6,7 +6,9 @@
 // Same argument rules, quality fill (the last value repeats, main.cpp:64-75),
 // same integer-millisecond timing line and "Success!" (main.cpp:11-41, 241),
 // same failure mode (usage, then the exception propagates).  BMP input
-// (-to_yuv) is outside the DCT path and reported as unsupported.
+// (main.cpp:100-136):
+//   myyuv_cli in.bmp -info
+//   myyuv_cli in.bmp -to_yuv IYUV -o out.myyuv   (conversion on the GPU, K7)
 #include <chrono>
 #include <cstring>
 #include <fstream>
@@ -33,6 +35,8 @@ void usage() {
             << "  myyuv_cli IMAGE.myyuv -info\n"
             << "  myyuv_cli IMAGE.myyuv -compress DCT Q [Q [Q]] -o OUT.myyuv   (Q in 1..100, per plane Y U V)\n"
             << "  myyuv_cli IMAGE.myyuv -decompress -o OUT.myyuv\n"
+            << "  myyuv_cli IMAGE.bmp -info\n"
+            << "  myyuv_cli IMAGE.bmp -to_yuv IYUV -o OUT.myyuv\n"
             << "\nYUV formats:\nIYUV\n\nCompression formats for YUV:\nDCT\n"
             << "\nExample:\n  myyuv_cli image.myyuv -compress DCT 50 -o image-DCT-50.myyuv\n";
 }
@@ -118,6 +122,42 @@ int run_yuv(const myyuv::YUV& yuv, size_t a, const std::vector<std::string>& arg
   return 1;
 }
 
+int run_bmp(const myyuv::BMP& bmp, size_t a, const std::vector<std::string>& args) {
+  const std::string& cmd = args[a];
+  if (cmd == "-info") {
+    const auto& h = bmp.header;
+    std::cout << "Type: " << h.type[0] << h.type[1] << '\n'
+              << "File size: " << h.file_size << '\n'
+              << "Data size: " << h.width * h.height * h.bit_count / 8 << '\n'
+              << "Width: " << h.width << '\n'
+              << "Height: " << h.height << '\n'
+              << "Bit count: " << h.bit_count << '\n'
+              << "Valid: " << bmp.isValid() << '\n';
+    return 0;
+  }
+  if (cmd == "-to_yuv") {
+    if (args.size() != a + 4) {
+      std::cout << "Invalid arguments amount. " << (a + 4) << " is required\n";
+      usage();
+      return 1;
+    }
+    if (args[a + 1] != "IYUV") throw std::runtime_error("Format is not registered: " + args[a + 1]);
+    if (args[a + 2] != "-o") {
+      std::cout << (a + 2) << " argument must be `-o` instead of " << args[a + 2] << '\n';
+      usage();
+      return 1;
+    }
+    myyuv::YUV out;
+    const float ms = elapsed_ms([&] { out = myyuv::YUV(bmp, myyuv::YUV::FourccFormats::IYUV); });
+    std::cout << "BMP to YUV (" << args[a + 1] << ") : " << ms << " ms\n";
+    out.dump(args[a + 3]);
+    return 0;
+  }
+  std::cout << "Invalid command " << cmd << '\n';
+  usage();
+  return 1;
+}
+
 int run(int argc, char* argv[]) {
   if (argc <= 2) {
     usage();
@@ -135,7 +175,7 @@ int run(int argc, char* argv[]) {
   if (magic[0] == 'Y' && magic[1] == 'U') {
     rc = run_yuv(myyuv::YUV(path), 2, args);
   } else if (magic[0] == 'B' && magic[1] == 'M') {
-    throw std::runtime_error("BMP input is not handled by the MI355X build (DCT path only): " + path);
+    rc = run_bmp(myyuv::BMP(path), 2, args);
   } else {
     throw std::runtime_error("Unknown image format (magic) " + path);
   }

@@ -57,6 +57,26 @@ std::unordered_map<YUV::FourccFormat, std::array<uint32_t, 2>> YUV::yuv_resoluti
     {FourccFormats::IYUV, {2, 2}},
 };
 
+// BMP -> IYUV (myyuv_yuv.cpp:88-128): K7 on the GPU (myyuv_gpu_bmp_to_iyuv);
+// the raw-image header as the reference's lambda sets it.
+std::unordered_map<YUV::FourccFormat, std::function<YUV(const BMP&)>> YUV::bmp_to_yuv_map = {
+    {FourccFormats::IYUV,
+     [](const BMP& bmp) -> YUV {
+       YUV res;
+       const uint32_t w = bmp.trueWidth(), h = bmp.trueHeight();
+       res.header.fourcc_format = FourccFormats::IYUV;
+       res.header.width = w;
+       res.header.height = h;
+       res.header.data_size = w * h * 3 / 2;
+       res.header.data_pos = sizeof(YUVHeader);
+       res.data = new uint8_t[res.header.data_size];
+       const int rc = myyuv_gpu_bmp_to_iyuv(t_codec.get(), bmp.data, bmp.header.width, bmp.header.height,
+                                            bmp.header.bit_count, res.data);
+       if (rc) fail(rc);
+       return res;
+     }},
+};
+
 // Registry: the [DCT][IYUV] entries are the drop-in (myyuv_yuv.cpp:130-160).
 std::unordered_map<YUV::Compression,
                    std::unordered_map<YUV::FourccFormat, std::function<YUV(const YUV&, const void*, uint32_t)>>>
@@ -84,6 +104,17 @@ std::unordered_map<YUV::Compression, std::unordered_map<YUV::FourccFormat, std::
 };
 
 YUV::YUV(const std::string& path) { load(path); }
+
+YUV::YUV(const BMP& bmp, FourccFormat format) { load(bmp, format); }
+
+// myyuv_yuv.cpp:512-523
+void YUV::load(const BMP& bmp, FourccFormat format) {
+  if (!bmp.isValid()) throw std::runtime_error("BMP is invalid");
+  auto it = bmp_to_yuv_map.find(format);
+  if (it == bmp_to_yuv_map.end()) throw std::runtime_error("Incorrect format");
+  YUV tmp = it->second(bmp);
+  *this = std::move(tmp);
+}
 
 YUV::YUV(const YUV& yuv) { *this = yuv; }
 

@@ -3,8 +3,9 @@
 // DCT path: the 64-byte header, load/dump, plane geometry, and the codec
 // registry (compress_map / decompress_map, myyuv_yuv.hpp:111,116) whose
 // [DCT][IYUV] entries here run the HIP kernels through the C ABI
-// (include/myyuv_hip.h).  Out of scope: BMP input
-// (bmp_to_yuv_map, YUV(const BMP&)) and per-pixel access (getPixel).
+// (include/myyuv_hip.h), and BMP input (bmp_to_yuv_map[IYUV], YUV(const BMP&),
+// myyuv_yuv.hpp:106,143,343), whose colour conversion runs on the GPU too
+// (K7).  Out of scope: per-pixel access (getPixel).
 #pragma once
 
 #include <array>
@@ -12,6 +13,8 @@
 #include <functional>
 #include <string>
 #include <unordered_map>
+
+#include "myyuv_bmp.hpp"
 
 namespace myyuv {
 
@@ -55,6 +58,7 @@ class YUV {
   static std::unordered_map<FourccFormat, FormatGroup> yuv_format_group_map;
   static std::unordered_map<FourccFormat, std::array<uint8_t, max_planes>> yuv_order_planes_map;
   static std::unordered_map<FourccFormat, std::array<uint32_t, 2>> yuv_resolution_fraction_map;
+  static std::unordered_map<FourccFormat, std::function<YUV(const BMP&)>> bmp_to_yuv_map;
   static std::unordered_map<Compression,
                             std::unordered_map<FourccFormat, std::function<YUV(const YUV&, const void*, uint32_t)>>>
       compress_map;
@@ -63,6 +67,7 @@ class YUV {
 
   YUV() {}
   explicit YUV(const std::string& path);
+  explicit YUV(const BMP& bmp, FourccFormat format);
   YUV(const YUV& yuv);
   YUV& operator=(const YUV& yuv);
   YUV(YUV&& yuv) noexcept;
@@ -90,6 +95,7 @@ class YUV {
   YUV decompress() const;
   bool isCompressed() const noexcept { return getCompression() != Compressions::NONE; }
   void load(const std::string& path);
+  void load(const BMP& bmp, FourccFormat format);
   void dump(const std::string& path) const;
 };
 

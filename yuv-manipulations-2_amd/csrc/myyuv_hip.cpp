@@ -39,6 +39,8 @@ __global__ void k_compact(const uint32_t*, const uint8_t*, const uint32_t*, cons
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
                               uint4*, unsigned long long*);
+template <int BPP>
+__global__ void k_bmp_to_iyuv(const uint8_t*, uint32_t, uint32_t, uint32_t, uint8_t*);
 #ifdef MYYUV_STAMPS
 extern __device__ unsigned long long g_k2_stamps[40];
 extern __device__ uint32_t g_k2_wstamps[65536 * 8];
@@ -157,6 +159,7 @@ struct myyuv_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   DevBuf frame, coef, slots, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
+  DevBuf bmp;   // staged BMP pixels (host-buffer BMP -> IYUV)
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
   // chained scan (k_chain.hpp): per-tile status words tagged with the launch
@@ -451,6 +454,9 @@ const char* myyuv_hip_strerror(int code) {
     case MYYUV_E_BAD_CHUNK: return "Huffman bad chunk";
     case MYYUV_E_HIP: return "HIP runtime error";
     case MYYUV_E_NO_DEVICE: return "No HIP device available";
+    case MYYUV_E_BMP_INVALID: return "BMP is invalid";
+    case MYYUV_E_BMP_SIGN: return "Unaccounted width and height sign";
+    case MYYUV_E_BMP_UNSUPPORTED: return "BMP to IYUV needs 24 or 32 bits per pixel and even height";
     default: return "Unknown error";
   }
 }
@@ -501,7 +507,8 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff,  &c->tiles, &c->payload,
-                    &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink};
+                    &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
+                    &c->bmp};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -573,6 +580,80 @@ int myyuv_hip_reserve_batch(myyuv_hip_handle c, uint32_t w, uint32_t h, uint32_t
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   return reserve(c, G);
+}
+
+// ---- K7: BMP -> IYUV (myyuv_yuv.cpp:88-128 over myyuv_bmp.cpp:77-101) ----
+namespace {
+
+// The checks the conversion itself makes, in the reference's order:
+// YUV::load's isValid (width % 4 of isValidHeader; bit_count > 0), then
+// colorData's sign cases, then the bmp_to_yuv_map asserts (even size,
+// 32 bpp — 24 bpp converts the same way and is accepted).
+int bmp_check(int32_t width, int32_t height, uint16_t bit_count, uint32_t* W, uint32_t* H,
+              uint32_t* orient) {
+  const uint32_t aw = width < 0 ? 0u - (uint32_t)width : (uint32_t)width;
+  const uint32_t ah = height < 0 ? 0u - (uint32_t)height : (uint32_t)height;
+  if (aw % 4 != 0 || bit_count == 0) return MYYUV_E_BMP_INVALID;
+  if (width > 0 && height < 0)
+    *orient = 0;
+  else if (width < 0 && height > 0)
+    *orient = 1;
+  else if (width > 0 && height > 0)
+    *orient = 2;
+  else
+    return MYYUV_E_BMP_SIGN;
+  if ((bit_count != 24 && bit_count != 32) || ah % 2 != 0) return MYYUV_E_BMP_UNSUPPORTED;
+  if ((uint64_t)aw * ah * 4 > 0xFFFFFFFFull) return MYYUV_E_ARG;  // imageSize() is a u32
+  *W = aw;
+  *H = ah;
+  return 0;
+}
+
+int launch_bmp(myyuv_hip_ctx* c, const void* src, uint32_t W, uint32_t H, uint32_t orient,
+               uint16_t bits, void* dst, hipStream_t s) {
+  const uint32_t tiles = (W / 4) * (H / 2);
+  if (tiles == 0) return 0;
+  const uint32_t grid = std::min(ceil_div(tiles, 256), 8192u);
+  const uint8_t* in = static_cast<const uint8_t*>(src);
+  uint8_t* out = static_cast<uint8_t*>(dst);
+  return bits == 32 ? launch(c, MYYUV_K_BMP, k_bmp_to_iyuv<4>, dim3(grid), dim3(256), s, in, W, H, orient, out)
+                    : launch(c, MYYUV_K_BMP, k_bmp_to_iyuv<3>, dim3(grid), dim3(256), s, in, W, H, orient, out);
+}
+
+}  // namespace
+
+int myyuv_gpu_bmp_to_iyuv_device(myyuv_hip_handle c, const void* d_bmp, int32_t width, int32_t height,
+                                 uint16_t bit_count, void* d_iyuv, void* stream) {
+  if (!c || !d_bmp || !d_iyuv) return MYYUV_E_ARG;
+  uint32_t W = 0, H = 0, orient = 0;
+  int e = bmp_check(width, height, bit_count, &W, &H, &orient);
+  if (e) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  return launch_bmp(c, d_bmp, W, H, orient, bit_count, d_iyuv, s);
+}
+
+int myyuv_gpu_bmp_to_iyuv(myyuv_hip_handle c, const uint8_t* bmp_data, int32_t width, int32_t height,
+                          uint16_t bit_count, uint8_t* iyuv) {
+  if (!c || !bmp_data || !iyuv) return MYYUV_E_ARG;
+  uint32_t W = 0, H = 0, orient = 0;
+  int e = bmp_check(width, height, bit_count, &W, &H, &orient);
+  if (e) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  const size_t in_bytes = (size_t)W * H * (bit_count / 8), out_bytes = (size_t)W * H * 3 / 2;
+  if (in_bytes == 0) return 0;
+  if (c->bmp.grow(in_bytes) || c->frame.grow(out_bytes)) return MYYUV_E_HIP;
+  if (hipMemcpyAsync(c->bmp.p, bmp_data, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return MYYUV_E_HIP;
+  if ((e = launch_bmp(c, c->bmp.p, W, H, orient, bit_count, c->frame.p, s))) return e;
+  if (hipMemcpyAsync(iyuv, c->frame.p, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return MYYUV_E_HIP;
+  if (c->prof) drain_profile(c);
+  return 0;
 }
 
 int myyuv_hip_sync_status(myyuv_hip_handle c, void* stream, int64_t* bad_block) {

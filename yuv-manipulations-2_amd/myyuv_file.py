@@ -66,3 +66,50 @@ class YUVFile:
     # ... and of decompress_DCT_planar (DCT.cpp:446-453)
     def decompressed(self, iyuv):
         return YUVFile(self.fourcc, self.width, self.height, NONE, b"", iyuv, self.unused)
+
+
+# ---- BMP input (myyuv_bmp.hpp:8-39, myyuv_bmp.cpp:141-166) ----
+BMP_HEADER = struct.Struct("<2sIHHIIiiHHIIiiII")  # 54 bytes, #pragma pack(1)
+BMP_COLOR = struct.Struct("<IIIII64s")            # 84 bytes (BMPColorHeader)
+
+
+class BMPFile:
+    """BMP::load: the 54-byte header, the colour header for 32-bit images,
+    then imageSize() = |w|*|h|*bit_count/8 bytes from data_pos."""
+
+    def __init__(self, width, height, bit_count, data, header=None, color=None):
+        self.width, self.height, self.bit_count = width, height, bit_count
+        self.data = bytes(data)
+        self.header = header
+        self.color = color or (0x00FF0000, 0x0000FF00, 0x000000FF, 0xFF000000, 0x73524742)
+
+    @classmethod
+    def load(cls, path_or_bytes):
+        b = path_or_bytes if isinstance(path_or_bytes, (bytes, bytearray)) else open(path_or_bytes, "rb").read()
+        hdr = BMP_HEADER.unpack(b[:54])
+        (typ, _fsz, _r1, _r2, dpos, hsz, w, h, _pl, bits, comp, _sz, _xp, _yp, cu, ci) = hdr
+        color = None
+        if bits == 32:
+            color = BMP_COLOR.unpack(b[54:54 + 84])[:5]
+        size = abs(w) * abs(h) * bits // 8
+        return cls(w, h, bits, b[dpos:dpos + size], hdr, color)
+
+    def is_valid_header(self):
+        """BMP::isValidHeader (myyuv_bmp.cpp:125-139)."""
+        typ, hsz, comp, cu, ci = (self.header[0], self.header[5], self.header[10], self.header[14],
+                                  self.header[15]) if self.header else (b"BM", 40, 0, 0, 0)
+        r, g, bl, a, cs = self.color
+        return (typ == b"BM" and self.width % 4 == 0 and self.bit_count > 0 and hsz > 0
+                and comp in (0, 3) and cu == 0 and ci == 0 and r == 0x00FF0000 and g == 0x0000FF00
+                and bl == 0x000000FF and a in (0xFF000000, 0) and cs == 0x73524742)
+
+    def dumps(self):
+        """BMP::dump layout (myyuv_bmp.cpp:168-179), for synthetic test images."""
+        bits = self.bit_count
+        dpos = 54 + (84 if bits == 32 else 0)
+        size = len(self.data)
+        out = BMP_HEADER.pack(b"BM", dpos + size, 0, 0, dpos, 124 if bits == 32 else 40, self.width,
+                              self.height, 1, bits, 3 if bits == 32 else 0, 0, 0, 0, 0, 0)
+        if bits == 32:
+            out += BMP_COLOR.pack(*self.color, b"\0" * 64)
+        return out + self.data

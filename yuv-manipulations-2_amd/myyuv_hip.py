@@ -17,11 +17,12 @@ OK = 0
 E_ARG, E_QUALITY, E_WIDTH, E_HEIGHT, E_CAPACITY = 1, 2, 3, 4, 5
 E_DCTYUV_SIZE, E_PLANE_SIZE, E_PLANE_NBLK, E_PLANE_CONTENT = 6, 7, 8, 9
 E_BAD_CODE, E_UNKNOWN_SYMBOL, E_BAD_CHUNK, E_HIP, E_NO_DEVICE = 10, 11, 12, 13, 14
+E_BMP_INVALID, E_BMP_SIGN, E_BMP_UNSUPPORTED = 15, 16, 17
 
 KERNELS = ["fdct_quant", "huff_encode", "scan_tiles", "compact", "parse", "huff_decode",
-           "dequant_idct", "huff_encode_wide", "scan_sums", "huff_encode_wave"]
+           "dequant_idct", "huff_encode_wide", "scan_sums", "huff_encode_wave", "bmp_to_iyuv"]
 (K_FDCT, K_HUFF_ENC, K_SCAN, K_COMPACT, K_PARSE, K_HUFF_DEC, K_IDCT, K_HUFF_WIDE,
- K_SCAN_SUMS, K_HUFF_WAVE) = range(10)
+ K_SCAN_SUMS, K_HUFF_WAVE, K_BMP) = range(11)
 
 # the exported symbols include/myyuv_hip.h declares (checked by the CPU tests)
 EXPORTS = [
@@ -30,7 +31,7 @@ EXPORTS = [
     "myyuv_gpu_dct_compress_device", "myyuv_gpu_dct_decompress_device", "myyuv_hip_sync_status",
     "myyuv_hip_profile", "myyuv_hip_profile_kernels", "myyuv_hip_kernel_stats", "myyuv_gpu_fdct_blocks",
     "myyuv_gpu_huff_encode_blocks", "myyuv_hip_reserve_batch", "myyuv_gpu_dct_compress_batch_device",
-    "myyuv_gpu_dct_decompress_batch_device",
+    "myyuv_gpu_dct_decompress_batch_device", "myyuv_gpu_bmp_to_iyuv", "myyuv_gpu_bmp_to_iyuv_device",
 ]
 
 _lib = None
@@ -95,6 +96,9 @@ def load():
     L.myyuv_gpu_fdct_blocks.argtypes = [vp, u8p, u32, ctypes.POINTER(ctypes.c_float),
                                         ctypes.POINTER(ctypes.c_int16)]
     L.myyuv_gpu_huff_encode_blocks.argtypes = [vp, ctypes.POINTER(ctypes.c_int16), u32, u8p, u8p]
+    i32 = ctypes.c_int32
+    L.myyuv_gpu_bmp_to_iyuv.argtypes = [vp, u8p, i32, i32, ctypes.c_uint16, u8p]
+    L.myyuv_gpu_bmp_to_iyuv_device.argtypes = [vp, vp, i32, i32, ctypes.c_uint16, vp, vp]
     _lib = L
     return L
 
@@ -164,6 +168,26 @@ class Codec:
         if rc:
             raise CodecError(rc, bad.value)
         return out.tobytes()
+
+    def bmp_to_iyuv(self, bmp_data, width, height, bit_count):
+        """BMP::data (as stored; signed header width/height) -> IYUV bytes,
+        as YUV(const BMP&, IYUV) (myyuv_yuv.cpp:88-128)."""
+        src = np.ascontiguousarray(np.frombuffer(memoryview(bmp_data).cast("B"), np.uint8))
+        W, H = abs(int(width)), abs(int(height))
+        if src.size < W * H * (bit_count // 8):
+            raise ValueError("pixel array smaller than |w|*|h|*bit_count/8")
+        out = np.empty(max(1, W * H * 3 // 2), np.uint8)
+        rc = load().myyuv_gpu_bmp_to_iyuv(self._h, _u8(src), int(width), int(height), int(bit_count),
+                                          _u8(out))
+        if rc:
+            raise CodecError(rc)
+        return out[: W * H * 3 // 2].tobytes()
+
+    def bmp_to_iyuv_device(self, d_bmp, width, height, bit_count, d_iyuv, stream=None):
+        rc = load().myyuv_gpu_bmp_to_iyuv_device(self._h, d_bmp, int(width), int(height),
+                                                 int(bit_count), d_iyuv, stream)
+        if rc:
+            raise CodecError(rc)
 
     # -- device-resident API (pointers are device addresses, e.g. torch data_ptr) --
     def reserve(self, w, h):
