@@ -136,10 +136,7 @@ __device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uin
 }
 
 // Compaction: one workgroup = up to 256 consecutive blocks of one plane of
-// frame blockIdx.y.
-// Chunks are OR-ed into an LDS image aligned to the stream's dword grid, then
-// written with dword stores (edge words byte by byte: they are shared with the
-// neighbouring workgroups' bytes).
+// frame blockIdx.y, one lane per block (chunk).
 __global__ __launch_bounds__(256) void k_compact(const uint32_t* __restrict__ slots,
                                                 const uint8_t* __restrict__ sizes,
                                                 const uint32_t* __restrict__ local_off,
@@ -148,7 +145,6 @@ __global__ __launch_bounds__(256) void k_compact(const uint32_t* __restrict__ sl
                                                 uint8_t* __restrict__ out, uint32_t cap,
                                                 uint32_t* __restrict__ out_size,
                                                 unsigned long long* __restrict__ err) {
-  __shared__ uint32_t img[(256 * kMaxChunk) / 4 + 2];
   // frame blockIdx.y of the batch: slots / sizes at batch-global block
   // gbase + g, its scan, its output slot of `cap` bytes
   const uint32_t f = blockIdx.y, gbase = f * G.cum[3];
@@ -187,45 +183,48 @@ __global__ __launch_bounds__(256) void k_compact(const uint32_t* __restrict__ sl
   if (total > cap) return;
 
   const uint32_t g = g0 + threadIdx.x;
-  const bool live = g < g1;
-  const uint64_t cbase = 12ull + 8ull * (p + 1) + G.cum[p + 1];  // + off[g]
-  const uint32_t off0 = scanned(local_off, tile_pre, g0);
-  const uint64_t start = cbase + off0;
-  const uint32_t end_off = scanned(local_off, tile_pre, g1 - 1) + sizes[g1 - 1];
-  const uint64_t end = cbase + end_off;
-  const uint64_t astart = start & ~3ull;
-  const uint32_t nwords = (uint32_t)((end - astart + 3) >> 2);
-  for (uint32_t i = threadIdx.x; i < nwords; i += 256) img[i] = 0;
-  __syncthreads();
-
-  if (live) {
-    const uint32_t s = sizes[g];
-    out[12ull + 8ull * (p + 1) + plane_pre + g] = (uint8_t)s;  // chunk_size[k]
-    const uint32_t lo = (uint32_t)(start - astart) + (scanned(local_off, tile_pre, g) - off0);
-    const uint32_t ga = gbase + g;
-    const uint32_t* slot = slots + (size_t)(ga / kWave) * (kSlotWords * kWave) + (ga % kWave);
-    const uint32_t nw = (s + 3) >> 2;
-    const uint32_t sh = (lo & 3) * 8;
-    for (uint32_t j = 0; j < nw; j++) {
-      const uint32_t d = slot[j * kWave];
-      const uint32_t wi = (lo >> 2) + j;
-      atomicOr(&img[wi], d << sh);
-      if (sh) atomicOr(&img[wi + 1], d >> (32 - sh));
-    }
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nwords; i += 256) {
-    const uint64_t a = astart + 4ull * i;
-    const uint32_t w = img[i];
-    if (a >= start && a + 4 <= end) {
-      *reinterpret_cast<uint32_t*>(out + a) = w;
-    } else {
-      for (int k = 0; k < 4; k++) {
-        const uint64_t b = a + k;
-        if (b >= start && b < end) out[b] = (uint8_t)(w >> (8 * k));
+  if (g >= g1) return;
+  const uint32_t sz = sizes[g];
+  out[12ull + 8ull * (p + 1) + plane_pre + g] = (uint8_t)sz;  // chunk_size[k]
+  // The chunk's bytes [pos, end) go straight to the stream: the image words
+  // strictly inside the range are this lane's alone (dword stores); the first
+  // and last words can hold a neighbour's bytes, so only this chunk's bytes of
+  // them are stored (byte stores: no read-modify-write, no atomics, no LDS).
+  // Slot words are loaded 8 at a time with no predication (a slot is always
+  // kSlotWords = 5 x 8 words long): one HBM round trip per batch.
+  const uint64_t pos = 12ull + 8ull * (p + 1) + G.cum[p + 1] + scanned(local_off, tile_pre, g);
+  const uint64_t end = pos + sz;
+  const uint64_t a0 = pos & ~3ull, al = (end - 1) & ~3ull;
+  const uint32_t sh = (uint32_t)(pos & 3) * 8;
+  const uint32_t ga = gbase + g;
+  const uint32_t* slot = slots + (size_t)(ga / kWave) * (kSlotWords * kWave) + (ga % kWave);
+  const uint32_t nw = (sz + 3) >> 2;
+  if (nw == 0) return;  // (a chunk is at least 7 bytes; a corrupt size of 0 writes nothing)
+  auto edge = [&](uint64_t a, uint32_t v) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (a + k >= pos && a + k < end) out[a + k] = (uint8_t)(v >> (8 * k));
+  };
+  uint32_t carry = 0;  // bits of the previous slot word shifted past its stream word
+  for (uint32_t j0 = 0; j0 < nw; j0 += 8) {
+    uint32_t d[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) d[k] = slot[(j0 + k) * kWave];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t j = j0 + k;
+      if (j < nw) {
+        const uint32_t v = sh ? (d[k] << sh) | carry : d[k];
+        carry = sh ? d[k] >> (32 - sh) : 0u;
+        const uint64_t a = a0 + 4ull * j;
+        if (a == a0 || a == al)
+          edge(a, v);
+        else
+          *reinterpret_cast<uint32_t*>(out + a) = v;
       }
     }
   }
+  if (a0 + 4ull * nw == al) edge(al, carry);
 }
 
 }  // namespace myyuv_gpu
