@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -I$P/csrc -I$R/include"
 /opt/rocm/bin/hipcc $FLAGS "$@" -fgpu-rdc -c "$P/csrc/$STEM.hip" -o "$OUT/$STEM.o"
 OBJS="$OUT/$STEM.o"
-for k in k_transform k_huff_encode k_huff_decode k_stream myyuv_hip; do
+for k in k_transform k_huff_encode k_huff_decode k_stream k_color myyuv_hip; do
   [ "$k" = "$STEM" ] || OBJS="$OBJS $P/build/$k.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fgpu-rdc --hip-link -shared -o "$OUT/libmyyuv_hip.so" $OBJS

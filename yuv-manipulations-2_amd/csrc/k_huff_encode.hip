@@ -740,7 +740,7 @@ __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict
 //   coef: natural-order quads (codec_common.hpp);
 //   slots: [ceil(n/64)][40][64] u32; sizes: [n] u8.
 #ifndef MYYUV_K2_WAVES
-#define MYYUV_K2_WAVES 1
+#define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (a few spills; +2.6 % in the bench, tools/ab_bench.sh)
 #endif
 __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
                                                          uint32_t nblocks,
