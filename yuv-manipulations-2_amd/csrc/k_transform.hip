@@ -157,10 +157,18 @@ __device__ __forceinline__ uint32_t unit_stride() { return gridDim.x * 4u; }
 // Stage 2 of either transform for one lane's row pair: out[2v + h] =
 // sum_k P[2k + h] * B(v, k) (h = row 2q + h), k ascending, with
 // B(v, k) = D[v][k] (forward: T * D^T) or D[k][v] (inverse: U * D).
-template <bool kInverse>
+// kSkip: a step k whose P[2k], P[2k+1] are zero in every lane of the wave is
+// skipped (the sums start at +0 and a +-0 product leaves a sum unchanged, so
+// the result is bit-identical; see K6).
+template <bool kInverse, bool kSkip = false>
 __device__ __forceinline__ void dot_rows(const float (&P)[16], float (&out)[16]) {
+  if (kSkip) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) out[j] = 0.0f;
+  }
 #pragma unroll
   for (int k = 0; k < 8; k++) {
+    if (kSkip && !__any(P[2 * k] != 0.0f || P[2 * k + 1] != 0.0f)) continue;
     float pr[16];
 #pragma unroll
     for (int v = 0; v < 8; v++) {
@@ -169,7 +177,7 @@ __device__ __forceinline__ void dot_rows(const float (&P)[16], float (&out)[16])
       pr[2 * v + 1] = P[2 * k + 1] * d;
     }
 #pragma unroll
-    for (int j = 0; j < 16; j++) out[j] = k == 0 ? pr[j] : out[j] + pr[j];
+    for (int j = 0; j < 16; j++) out[j] = (k == 0 && !kSkip) ? pr[j] : out[j] + pr[j];
     fence16(out);
   }
 }
@@ -430,9 +438,18 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
 #else
     // ---- dequantise (DCT.cpp:331) and stage 1: U[i][j] = sum_k D[k][i] * Z[k][j],
     // j in {2q, 2q+1} (squareMatrixMulT2<8>(DCT, Z), DCT.cpp:256-266)
+    // Quantised blocks are sparse: a coefficient row k that is zero in all 16
+    // blocks of the unit (61 % of the (unit, k) pairs of the bench frame)
+    // contributes only +-0 products, and a sum that starts at +0 (as the
+    // reference's does, DCT.cpp:259-263) is unchanged by them — so the wave
+    // skips that step outright, bit-exactly.  Stage 2 skips the zero columns
+    // of Z the same way (U's column k is zero exactly when Z's is).
     float Um[16];  // Um[2i + h] = U[i][2q + h]
 #pragma unroll
+    for (int j = 0; j < 16; j++) Um[j] = 0.0f;
+#pragma unroll
     for (int k = 0; k < 8; k++) {
+      if (!__any(zc[k] != 0u)) continue;
       const float z0 = (float)(int16_t)zc[k] * qk[2 * k];
       const float z1 = (float)(int16_t)(zc[k] >> 16) * qk[2 * k + 1];
       float pr[16];
@@ -442,7 +459,7 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
         pr[2 * i + 1] = c_dct[k * 8 + i] * z1;
       }
 #pragma unroll
-      for (int j = 0; j < 16; j++) Um[j] = k == 0 ? pr[j] : Um[j] + pr[j];
+      for (int j = 0; j < 16; j++) Um[j] = Um[j] + pr[j];
       fence16(Um);
     }
 
@@ -453,7 +470,7 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
     // ---- stage 2: R[i][v] = sum_k U[i][k] * D[k][v] (squareMatrixMul<8>(U, DCT)),
     // then clamp(roundf(R) + 128) (DCT.cpp:358-362)
     float S[16];  // S[2v + h] = R[2q + h][v]
-    dot_rows<true>(P, S);
+    dot_rows<true, true>(P, S);
     uint32_t px[16];  // low byte = pixel
     float mt = 0.0f;  // max |s' - rint(s')| of the lane: 0.5 means an exact tie
 #pragma unroll
