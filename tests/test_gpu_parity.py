@@ -97,6 +97,36 @@ def test_noise_long_overflow_list(codec, oracle, q):
     assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q)
 
 
+def sparse_basis_frame(w, h, seed):
+    """Every 8x8 block is 128 + a * basis(u, v) for a random (u, v) (zero for a
+    quarter of the blocks): after quantisation mostly one or two nonzero
+    coefficients per block, in random rows and columns, so K6's per-unit
+    zero-row / zero-column skipping meets every pattern of live steps."""
+    rng = np.random.default_rng(seed)
+    n = np.arange(8)
+    C = np.cos((2 * n[None, :] + 1) * n[:, None] * np.pi / 16)  # C[u][x]
+    out = np.empty(w * h * 3 // 2, np.uint8)
+    planes = [(0, w, h), (w * h, w // 2, h // 2), (w * h * 5 // 4, w // 2, h // 2)]
+    for off, pw, ph in planes:
+        nb = (pw // 8) * (ph // 8)
+        u, v = rng.integers(0, 8, nb), rng.integers(0, 8, nb)
+        amp = rng.choice([0.0, 20.0, 60.0, 110.0], nb) * rng.choice([-1.0, 1.0], nb)
+        blk = 128 + amp[:, None, None] * C[u][:, :, None] * C[v][:, None, :]
+        img = np.clip(np.rint(blk), 0, 255).astype(np.uint8)
+        img = img.reshape(ph // 8, pw // 8, 8, 8).transpose(0, 2, 1, 3).reshape(ph, pw)
+        out[off:off + pw * ph] = img.reshape(-1)
+    return out.tobytes()
+
+
+@pytest.mark.parametrize("q", [(50, 50, 50), (90, 90, 90), (5, 20, 100)])
+def test_sparse_blocks_vs_oracle(codec, oracle, q):
+    w, h = 1024, 512
+    fr = sparse_basis_frame(w, h, sum(q))
+    pay = oracle.compress(fr, w, h, q)
+    assert codec.compress(fr, w, h, q) == pay
+    assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q)
+
+
 @pytest.mark.parametrize("wh", [(16, 16), (48, 16), (16, 48), (1008, 16), (144, 272)])
 def test_odd_geometries(codec, oracle, wh):
     w, h = wh

@@ -5,8 +5,11 @@ compressed streams gathered to rank 0 — the one exchange step of the path.
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on
 the GPU box; "gloo" for the CPU tests).  The gather is two collectives:
   1. all_gather of the per-frame u32 payload sizes (fixed shape),
-  2. exact-size point-to-point transfers of the payloads to rank 0, batched
-     in one group (batch_isend_irecv), so no rank pads to a worst case.
+  2. one exact-size point-to-point transfer per rank to rank 0: each rank
+     packs its streams back to back (no padding to a worst case), rank 0
+     posts one receive per rank (batch_isend_irecv) and splits the buffers
+     by the gathered sizes.  A few large messages keep every xGMI link busy;
+     one message per frame would be thousands of small RCCL operations.
 The codec itself is a callable, so the same driver runs the HIP codec
 (myyuv_hip, device tensors) or, in tests, the CPU restatement (host tensors).
 """
@@ -33,23 +36,31 @@ def gather_streams(dist, payloads, sizes, n_frames, world, rank, device):
     parts = [torch.empty(per, dtype=torch.int32, device=device) for _ in range(world)]
     dist.all_gather(parts, mine)
     hs = [p.cpu().tolist() for p in parts]
-    ops = []
-    out = None
-    if rank == 0:
-        out = [None] * n_frames
-        for i, f in enumerate(shard(n_frames, world, 0)):
-            out[f] = payloads[i][: hs[0][i]]
-        for r in range(1, world):
-            for i, f in enumerate(shard(n_frames, world, r)):
-                buf = torch.empty(hs[r][i], dtype=torch.uint8, device=device)
-                out[f] = buf
-                ops.append(dist.P2POp(dist.irecv, buf, r))
-    else:
-        for i in range(len(payloads)):
-            ops.append(dist.P2POp(dist.isend, payloads[i][: hs[rank][i]].contiguous(), 0))
+    counts = [len(shard(n_frames, world, r)) for r in range(world)]
+    totals = [sum(hs[r][: counts[r]]) for r in range(world)]
+    if rank != 0:
+        if totals[rank] > 0:
+            packed = torch.cat([payloads[i][: hs[rank][i]] for i in range(counts[rank])])
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed, 0)]):
+                req.wait()
+        return None
+    out = [None] * n_frames
+    for i, f in enumerate(shard(n_frames, world, 0)):
+        out[f] = payloads[i][: hs[0][i]]
+    bufs, ops = {}, []
+    for r in range(1, world):
+        if totals[r] > 0:
+            bufs[r] = torch.empty(totals[r], dtype=torch.uint8, device=device)
+            ops.append(dist.P2POp(dist.irecv, bufs[r], r))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    for r in range(1, world):
+        off = 0
+        for i, f in enumerate(shard(n_frames, world, r)):
+            n = hs[r][i]
+            out[f] = bufs[r][off:off + n] if n else torch.empty(0, dtype=torch.uint8, device=device)
+            off += n
     return out
 
 
