@@ -284,6 +284,7 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
                                                    FrameGeom G, uint32_t tiles_p0,
                                                    uint32_t tiles_p1,
                                                    uint4* __restrict__ coef,
+                                                   uint8_t* __restrict__ rmask,
                                                    unsigned long long* __restrict__ err) {
   __shared__ uint4 stq[kStageQuads];
   // frame blockIdx.y of the batch: its stream slot, descriptor and scan;
@@ -404,10 +405,21 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
   if (ok && code) record_error(err, 2ull * (gbase + g) + 1, code);
 
   // ---- natural-order words to the quad layout (1 KiB contiguous per store)
-  if (live && !direct) {
+  // Only the nonzero rows are stored; bit c of the block's row mask says
+  // whether row c holds a nonzero coefficient, and K6 reads just those.
+  // decode_general wrote all 64 coefficients itself: mask 0xFF.
+  if (live) {
+    uint32_t m = 0xFFu;
+    if (!direct) {
+      m = 0;
 #pragma unroll
-    for (int c = 0; c < 8; c++)
-      coef[coef_quad(gbase + g, c)] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
+      for (int c = 0; c < 8; c++) {
+        const bool nz = (nw[4 * c] | nw[4 * c + 1] | nw[4 * c + 2] | nw[4 * c + 3]) != 0u;
+        m |= nz ? 1u << c : 0u;
+        if (nz) coef[coef_quad(gbase + g, c)] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
+      }
+    }
+    rmask[gbase + g] = (uint8_t)m;
   }
 }
 

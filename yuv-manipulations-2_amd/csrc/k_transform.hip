@@ -230,16 +230,21 @@ __device__ __forceinline__ void stage_tables(const float* __restrict__ src, floa
   __syncthreads();
 }
 
-// Coefficient quads 2q, 2q+1 (rows 2q, 2q+1) of the lane's block in unit u
-// (the last block of the plane past its end).
-__device__ __forceinline__ void load_quads(const uint4* __restrict__ coef, const FrameGeom& G,
-                                           uint32_t ua, uint32_t b, uint32_t q, uint4& a, uint4& c) {
+__device__ __forceinline__ uint32_t unit_block(const FrameGeom& G, uint32_t ua, uint32_t b) {
   const uint32_t f = div_magic(ua, G.umag);
   const Unit U = unit_of(G, ua - f * G.ucum[3]);
   const uint32_t local = U.local0 + b;
-  const uint32_t g = f * G.cum[3] + U.cum + (local < U.nb ? local : U.nb - 1);
-  a = coef[coef_quad(g, 2 * q)];
-  c = coef[coef_quad(g, 2 * q + 1)];
+  return f * G.cum[3] + U.cum + (local < U.nb ? local : U.nb - 1);
+}
+
+// Quads 2q, 2q+1 of block g; rows whose mask bit is clear read a zero quad
+// (always issued: unconditional loads keep the vmcnt pipelining)
+__device__ __forceinline__ void load_quads(const uint4* __restrict__ coef, const uint4* __restrict__ zq,
+                                           uint32_t g, uint32_t q, uint32_t m, uint4& a, uint4& c) {
+  const uint4* pa = (m >> (2 * q)) & 1u ? coef + coef_quad(g, 2 * q) : zq;
+  const uint4* pc = (m >> (2 * q + 1)) & 1u ? coef + coef_quad(g, 2 * q + 1) : zq;
+  a = *pa;
+  c = *pc;
 }
 
 }  // namespace
@@ -388,7 +393,9 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
 // K6: int16 coefficients (natural order, quad layout) -> u8 planes.
 // DCT.cpp:330-334 (dequant, squareMatrixMulT2, squareMatrixMul), :358-362
 // (roundf, +128, clamp).
-__global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4* __restrict__ coef, FrameGeom G,
+__global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4* __restrict__ coef,
+                                                     const uint8_t* __restrict__ rmask,
+                                                     const uint4* __restrict__ zq, FrameGeom G,
                                                      const QTables* __restrict__ qt,
                                                      uint8_t* __restrict__ frame, uint4* __restrict__ sink) {
   __shared__ float tile[4][kXfUnit * kTile];
@@ -401,7 +408,12 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
   const uint32_t nall = G.ucum[3] * G.nframes, stride = unit_stride();
   uint32_t ua = first_unit();
   uint4 na = make_uint4(0, 0, 0, 0), nc = na;
-  if (ua < nall) load_quads(coef, G, ua, b, q, na, nc);
+  uint32_t un = ua + stride < nall ? ua + stride : ua, nm = 0;
+  if (ua < nall) {
+    const uint32_t g0 = unit_block(G, ua, b);
+    load_quads(coef, zq, g0, q, rmask[g0], na, nc);
+    nm = rmask[unit_block(G, un, b)];
+  }
   sink[lane] = make_uint4(0, 0, 0, 0);  // see K1
   sink[64 + lane] = make_uint4(0, 0, 0, 0);
 
@@ -413,7 +425,9 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
     // dwords of its tile); the next unit's quads in flight
     *reinterpret_cast<uint4*>(tw + 8 * q) = na;
     *reinterpret_cast<uint4*>(tw + 8 * q + 4) = nc;
-    load_quads(coef, G, ua + stride < nall ? ua + stride : ua, b, q, na, nc);  // unconditional: see K1
+    load_quads(coef, zq, unit_block(G, un, b), q, nm, na, nc);  // unconditional: see K1
+    un = un + stride < nall ? un + stride : un;
+    nm = rmask[unit_block(G, un, b)];
     wave_sync();
     // (Z[k][2q], Z[k][2q+1]) = word k*4 + q
     uint32_t zc[8];

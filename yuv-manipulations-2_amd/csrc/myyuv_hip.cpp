@@ -23,7 +23,8 @@
 
 namespace myyuv_gpu {
 __global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint4*, uint32_t*);
-__global__ void k_dequant_idct(const uint4*, FrameGeom, const QTables*, uint8_t*, uint4*);
+__global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*,
+                               uint4*);
 __global__ void k_huff_encode(const uint4*, uint32_t, uint32_t*, uint8_t*,
                               uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, uint32_t*, uint8_t*, const uint32_t*,
@@ -38,7 +39,7 @@ __global__ void k_compact(const uint32_t*, const uint8_t*, const uint32_t*, cons
                           unsigned long long*);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
-                              uint4*, unsigned long long*);
+                              uint4*, uint8_t*, unsigned long long*);
 template <int BPP>
 __global__ void k_bmp_to_iyuv(const uint8_t*, uint32_t, uint32_t, uint32_t, uint8_t*);
 #ifdef MYYUV_STAMPS
@@ -160,6 +161,8 @@ struct myyuv_hip_ctx {
   hipStream_t stream = nullptr;
   DevBuf frame, coef, slots, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
   DevBuf bmp;   // staged BMP pixels (host-buffer BMP -> IYUV)
+  DevBuf rmask; // per block: bit c = coefficient row c nonzero (K5 -> K6)
+  DevBuf zq;    // 256 zero bytes: K6's source for rows the mask says are zero
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
   // chained scan (k_chain.hpp): per-tile status words tagged with the launch
@@ -276,6 +279,11 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->coef.grow((size_t)nwaves * kCoefQuadsPerWave * 16);  // natural-order quads
   e |= c->slots.grow((size_t)nwaves * kSlotWords * kWave * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
+  e |= c->rmask.grow((size_t)nblk);
+  if (c->zq.n == 0) {
+    e |= c->zq.grow(256);
+    if (!e && hipMemset(c->zq.p, 0, 256) != hipSuccess) e |= MYYUV_E_HIP;
+  }
   e |= c->loff.grow((size_t)nblk * 4);
   e |= c->tiles.grow((size_t)nf * (ntiles + 1) * 4);
   e |= c->err.grow(8);
@@ -380,9 +388,10 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
   e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size,
               cap, (const StreamDesc*)desc, c->loff.as<const uint32_t>(),
-              c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<uint4>(), err);
+              c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<uint4>(), c->rmask.as<uint8_t>(), err);
   e |= launch(c, MYYUV_K_IDCT, k_dequant_idct, xf_grid(G, c->xf_resident[1]), dim3(256), s,
-              c->coef.as<const uint4>(), G, qt, static_cast<uint8_t*>(d_out), c->sink.as<uint4>());
+              c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G, qt,
+              static_cast<uint8_t*>(d_out), c->sink.as<uint4>());
   return e ? MYYUV_E_HIP : 0;
 }
 
@@ -508,7 +517,7 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff,  &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
-                    &c->bmp};
+                    &c->bmp,   &c->rmask, &c->zq};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
