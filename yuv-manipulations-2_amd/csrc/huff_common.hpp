@@ -114,10 +114,13 @@ constexpr uint8_t c_zz[64] = MYYUV_ZIGZAG;
 
 struct CoefRegs {
   uint32_t w[32];
-  __device__ __forceinline__ void load(const uint4* __restrict__ coef, uint32_t g) {
+  // rows whose bit in the block's row mask m (K1) is clear are zero: read
+  // from the zero buffer zq instead (the load is still issued)
+  __device__ __forceinline__ void load(const uint4* __restrict__ coef, const uint4* __restrict__ zq,
+                                       uint32_t g, uint32_t m) {
 #pragma unroll
     for (int c = 0; c < 8; c++) {
-      const uint4 v = coef[coef_quad(g, c)];
+      const uint4 v = *((m >> c) & 1u ? coef + coef_quad(g, c) : zq);
       w[4 * c] = v.x;
       w[4 * c + 1] = v.y;
       w[4 * c + 2] = v.z;

@@ -563,7 +563,8 @@ __device__ __forceinline__ void put_bits(uint32_t* img, uint32_t off, uint32_t v
   if (sh + nb > 32) atomicOr(&img[w + 1], v >> (32 - sh));
 }
 
-__device__ void encode_block_wave(const uint4* __restrict__ coef, uint32_t g, uint32_t* img,
+__device__ void encode_block_wave(const uint4* __restrict__ coef, const uint8_t* __restrict__ rmask, uint32_t g,
+                                  uint32_t* img,
                                   uint32_t* __restrict__ slots, uint8_t* __restrict__ sizes,
                                   uint32_t _wslot = 0) {
   const uint32_t lane = threadIdx.x;
@@ -573,8 +574,9 @@ __device__ void encode_block_wave(const uint4* __restrict__ coef, uint32_t g, ui
   WSTAMP(0);
   // ---- lane i: zig-zag position i (Huffman.cpp:176-182)
   const uint32_t nat = c_zz_lane[lane];
-  const uint32_t word =
-      reinterpret_cast<const uint32_t*>(coef)[coef_quad(g, nat >> 3) * 4u + ((nat >> 1) & 3u)];
+  const uint32_t word = (rmask[g] >> (nat >> 3)) & 1u  // row nat >> 3 is nonzero
+                            ? reinterpret_cast<const uint32_t*>(coef)[coef_quad(g, nat >> 3) * 4u + ((nat >> 1) & 3u)]
+                            : 0u;
   const int v = (int)(int16_t)(word >> (16 * (nat & 1)));
   const uint64_t nzm = __ballot(v != 0);
   int msz = nzm ? 64 - __clzll((long long)nzm) : 0;
@@ -718,6 +720,7 @@ __device__ void encode_block_wave(const uint4* __restrict__ coef, uint32_t g, ui
 // encode_block_wave); exits at once when the list is long (the lane pass
 // k_huff_encode_wide takes it).
 __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict__ coef,
+                                                        const uint8_t* __restrict__ rmask,
                                                         uint32_t* __restrict__ slots,
                                                         uint8_t* __restrict__ sizes,
                                                         const uint32_t* __restrict__ work,
@@ -726,7 +729,7 @@ __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict
   __shared__ uint32_t img[kSlotWords + 2];
   const uint32_t cnt = *work_count;
   if (cnt > limit) return;
-  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) encode_block_wave(coef, work[i], img, slots, sizes, i);
+  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) encode_block_wave(coef, rmask, work[i], img, slots, sizes, i);
 }
 
 // Fast pass over every block.  A workgroup takes kK2Group consecutive blocks,
@@ -743,6 +746,8 @@ __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict
 #define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (a few spills; +2.6 % in the bench, tools/ab_bench.sh)
 #endif
 __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
+                                                         const uint8_t* __restrict__ rmask,
+                                                         const uint4* __restrict__ zq,
                                                          uint32_t nblocks,
                                                          uint32_t* __restrict__ slots,
                                                          uint8_t* __restrict__ sizes,
@@ -750,16 +755,18 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
                                                          uint32_t* __restrict__ work_count) {
   constexpr int kWaves = kK2Group / kWave;
   __shared__ uint32_t s_g[kK2Group];
-  __shared__ uint8_t s_msz[kK2Group], s_cls[kK2Group];
+  __shared__ uint8_t s_msz[kK2Group], s_cls[kK2Group], s_rm[kK2Group];
   __shared__ uint32_t s_cnt[kWaves][kClassDead + 1];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // ---- classify
   const uint32_t g = blockIdx.x * kK2Group + tid;
   uint32_t cls = kClassDead;
   int msz = 0;
+  uint32_t rm = 0;
   if (g < nblocks) {
+    rm = rmask[g];
     CoefRegs R;
-    R.load(coef, g);
+    R.load(coef, zq, g, rm);
     msz = R.msz();
     cls = block_class(R, msz);
   }
@@ -782,6 +789,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   s_g[pos] = g;
   s_msz[pos] = (uint8_t)msz;
   s_cls[pos] = (uint8_t)cls;
+  s_rm[pos] = (uint8_t)rm;
   __syncthreads();
   // ---- encode: wave w takes sorted chunk w < kWaves/2 ? kWaves-1-w : w-kWaves/2
   const uint32_t chunk = wave < (uint32_t)kWaves / 2 ? kWaves - 1 - wave : wave - kWaves / 2;
@@ -801,7 +809,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   const unsigned long long _w0 = __builtin_amdgcn_s_memtime();
 #endif
   CoefRegs R;
-  R.load(coef, live ? mg : 0u);
+  R.load(coef, zq, live ? mg : 0u, live ? s_rm[e] : 0u);
   uint32_t* slot = slots + (size_t)(mg >> 6) * (kSlotWords * kWave) + (mg & 63);
   uint8_t* so = sizes + mg;
   bool ok = true;
@@ -830,6 +838,8 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
 // *work_count), 64 per workgroup; the grid is sized for the worst case, idle
 // groups exit.  Lists of at most `limit` blocks go to k_huff_encode_wave instead.
 __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict__ coef,
+                                                        const uint8_t* __restrict__ rmask,
+                                                        const uint4* __restrict__ zq,
                                                         uint32_t* __restrict__ slots,
                                                         uint8_t* __restrict__ sizes,
                                                         const uint32_t* __restrict__ work,
@@ -846,7 +856,7 @@ __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict
     const bool live = i < cnt;
     const uint32_t g = live ? work[i] : 0;
     CoefRegs R;
-    R.load(coef, g);
+    R.load(coef, zq, g, live ? rmask[g] : 0u);
     const int msz = live ? R.msz() : 0;
     const int wmsz = wave_max(msz);
     if (live) {

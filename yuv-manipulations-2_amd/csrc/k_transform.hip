@@ -253,8 +253,8 @@ __device__ __forceinline__ void load_quads(const uint4* __restrict__ coef, const
 // DCT.cpp:297-306 (gather, x - 128), :269-277 (applyDCTBlock).
 __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t* __restrict__ frame, FrameGeom G,
                                                    const QTables* __restrict__ qt,
-                                                   uint4* __restrict__ coef, uint4* __restrict__ sink,
-                                                   uint32_t* __restrict__ k2ctl) {
+                                                   uint4* __restrict__ coef, uint8_t* __restrict__ rmask,
+                                                   uint4* __restrict__ sink, uint32_t* __restrict__ k2ctl) {
   // K2's overflow count for the launch that follows in the stream (nullptr: none)
   if (k2ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *k2ctl = 0u;
   __shared__ float tile[4][kXfUnit * kTile];
@@ -273,6 +273,7 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
   // prefetch: the loop top then waits with vmcnt(2) on every path
   sink[lane] = make_uint4(0, 0, 0, 0);
   sink[64 + lane] = make_uint4(0, 0, 0, 0);
+  reinterpret_cast<uint8_t*>(sink + 128)[lane] = 0;
 
   for (; ua < nall; ua += stride) {
     const uint32_t f = div_magic(ua, G.umag);
@@ -383,8 +384,18 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
         *dhi = hi;
       }
 #else
-      *dlo = lo;
-      *dhi = hi;
+      // Row mask for K2 (bit c: row c has a nonzero coefficient), from the
+      // block's four lanes; an all-zero row is not stored (K2 reads masked-off
+      // rows from a zero buffer), which saves most of the 128 B per block of
+      // a q=50 frame twice (this write, K2's read).  Every lane still issues
+      // its three stores (the sink takes the skipped ones).
+      const bool nzl = (lo.x | lo.y | lo.z | lo.w) != 0u, nzh = (hi.x | hi.y | hi.z | hi.w) != 0u;
+      uint32_t rm = (nzl ? 1u << (2 * q) : 0u) | (nzh ? 2u << (2 * q) : 0u);
+      rm |= __shfl_xor(rm, 1, 64);
+      rm |= __shfl_xor(rm, 2, 64);
+      *(live ? rmask + g : reinterpret_cast<uint8_t*>(sink + 128) + lane) = (uint8_t)rm;
+      *(nzl ? dlo : sink + lane) = lo;
+      *(nzh ? dhi : sink + 64 + lane) = hi;
 #endif
     }
   }

@@ -22,14 +22,14 @@
 #include "myyuv_hip.h"
 
 namespace myyuv_gpu {
-__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint4*, uint32_t*);
+__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*);
 __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*,
                                uint4*);
-__global__ void k_huff_encode(const uint4*, uint32_t, uint32_t*, uint8_t*,
+__global__ void k_huff_encode(const uint4*, const uint8_t*, const uint4*, uint32_t, uint32_t*, uint8_t*,
                               uint32_t*, uint32_t*);
-__global__ void k_huff_encode_wave(const uint4*, uint32_t*, uint8_t*, const uint32_t*,
+__global__ void k_huff_encode_wave(const uint4*, const uint8_t*, uint32_t*, uint8_t*, const uint32_t*,
                                    const uint32_t*, uint32_t);
-__global__ void k_huff_encode_wide(const uint4*, uint32_t*, uint8_t*,
+__global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, uint32_t*, uint8_t*,
                                    const uint32_t*, const uint32_t*, uint32_t);
 __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
                              StreamDesc*, uint32_t*, uint32_t*, uint32_t, unsigned long long*,
@@ -287,7 +287,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->loff.grow((size_t)nblk * 4);
   e |= c->tiles.grow((size_t)nf * (ntiles + 1) * 4);
   e |= c->err.grow(8);
-  e |= c->sink.grow(128 * 16);
+  e |= c->sink.grow(192 * 16);  // K1/K6: 2 x 64 quads + K1's 64 mask bytes
   e |= c->psize.grow(4);
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
   e |= c->work.grow((size_t)nblk * 4 + 256);  // [0]: overflow count, then block ids
@@ -320,15 +320,15 @@ int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, uint32_t nf, hipStream_t
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
   const uint32_t limit = nf > 1 ? 0u : kWaveEncodeLimit;
   int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(ceil_div(nblk, kK2Group)), dim3(kK2Group), s,
-                 c->coef.as<const uint4>(), nblk, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
+                 c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), nblk, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
                  list, count);
   if (limit > 0)
     e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
-                c->coef.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
+                c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
                 (const uint32_t*)list, (const uint32_t*)count, limit);
   const uint32_t wide = ceil_div(nblk, kWave) < kWideGrid ? ceil_div(nblk, kWave) : kWideGrid;
   e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(wide), dim3(kWave), s,
-              c->coef.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
+              c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
               (const uint32_t*)list, (const uint32_t*)count, limit);
   return e;
 }
@@ -344,8 +344,8 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   unsigned long long* err = c->err.as<unsigned long long>();
   int e = 0;
   e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
-              static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->sink.as<uint4>(),
-              c->work.as<uint32_t>());
+              static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
+              c->sink.as<uint4>(), c->work.as<uint32_t>());
   if ((c->skip >> MYYUV_K_FDCT) & 1u)  // diagnostic skip: keep K1's reset of the overflow count
     e |= hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess;
   e |= launch_huff_encode(c, nblk * nf, nf, s);
@@ -842,13 +842,20 @@ int myyuv_debug_coef(myyuv_hip_handle c, int16_t* out, uint32_t n) {
   DeviceGuard g(c->device);
   const size_t nq = (size_t)ceil_div(n, kWave) * kCoefQuadsPerWave;
   if (nq * 16 > c->coef.n) return MYYUV_E_ARG;
+  if (n > c->rmask.n) return MYYUV_E_ARG;
   std::vector<uint4> img(nq);
+  std::vector<uint8_t> rm(n);
   if (hipStreamSynchronize(c->stream) != hipSuccess ||
-      hipMemcpy(img.data(), c->coef.p, nq * 16, hipMemcpyDeviceToHost) != hipSuccess)
+      hipMemcpy(img.data(), c->coef.p, nq * 16, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(rm.data(), c->rmask.p, n, hipMemcpyDeviceToHost) != hipSuccess)
     return MYYUV_E_HIP;
   for (uint32_t b = 0; b < n; b++)
-    for (uint32_t q = 0; q < 8; q++)
-      std::memcpy(out + (size_t)b * 64 + q * 8, &img[coef_quad(b, q)], 16);
+    for (uint32_t q = 0; q < 8; q++) {  // rows outside the row mask are zero (not stored)
+      if ((rm[b] >> q) & 1u)
+        std::memcpy(out + (size_t)b * 64 + q * 8, &img[coef_quad(b, q)], 16);
+      else
+        std::memset(out + (size_t)b * 64 + q * 8, 0, 16);
+    }
   return 0;
 }
 
@@ -884,17 +891,23 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
     return MYYUV_E_HIP;
   hipLaunchKernelGGL(k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), 0, s,
                      c->frame.as<const uint8_t>(), G, c->qtd.as<const QTables>(), c->coef.as<uint4>(),
-                     c->sink.as<uint4>(), (uint32_t*)nullptr);
+                     c->rmask.as<uint8_t>(), c->sink.as<uint4>(), (uint32_t*)nullptr);
   std::vector<uint32_t> words((size_t)ceil_div(nblocks, kWave) * kCoefQuadsPerWave * 4);
+  std::vector<uint8_t> rm(nblocks);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(words.data(), c->coef.p, words.size() * 4, hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
+      hipMemcpyAsync(rm.data(), c->rmask.p, nblocks, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return MYYUV_E_HIP;
   for (uint32_t g = 0; g < nblocks; g++) {
     int16_t nat[64];
-    for (uint32_t c4 = 0; c4 < 8; c4++)
-      std::memcpy(nat + 8 * c4, &words[(size_t)coef_quad(g, c4) * 4], 16);
+    for (uint32_t c4 = 0; c4 < 8; c4++) {  // rows K1 left out of the image (mask bit clear) are zero
+      if ((rm[g] >> c4) & 1u)
+        std::memcpy(nat + 8 * c4, &words[(size_t)coef_quad(g, c4) * 4], 16);
+      else
+        std::memset(nat + 8 * c4, 0, 16);
+    }
     for (int z = 0; z < 64; z++) coef_zz[(size_t)g * 64 + z] = nat[kZigzag[z]];
   }
   return 0;
@@ -925,6 +938,7 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
       std::memcpy(&words[(size_t)coef_quad(g, c4) * 4], nat + 8 * c4, 16);
   }
   if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemsetAsync(c->rmask.p, 0xFF, nblocks, s) != hipSuccess ||  // every row present
       hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess)  // K1 zeroes it in the codec path
     return MYYUV_E_HIP;
   if (launch_huff_encode(c, nblocks, 1, s)) return MYYUV_E_HIP;
