@@ -33,9 +33,11 @@ reference sources with OpenMP, kind "reference") — or the C restatement
 rank 0 at N=1 only, on a bounded sample of the same workload.
 
 N>1 (torch.distributed.run, one rank per GPU): frames are sharded one per GPU
-(weak scaling); at the end of the timed region rank 0 gathers every rank's
-compressed streams over RCCL (sizes all-gathered first, then exact-size
-point-to-point transfers): the batch configuration's exchange step.
+(weak scaling); inside the timed region rank 0 gathers every rank's
+compressed streams over RCCL (batch.ChunkedGather: per chunk of frames the
+sizes are all-gathered, then one packed exact-size point-to-point message per
+rank, overlapped with the following chunks' compression): the batch
+configuration's exchange step.
 """
 import argparse
 import hashlib
@@ -76,6 +78,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4,
                     help="frames per launch (the batch entry points): each kernel covers this "
                          "many frames")
+    ap.add_argument("--gather-chunk", type=int, default=32,
+                    help="N>1: frames per chunk of the overlapped gather to rank 0")
     ap.add_argument("--no-side", action="store_true",
                     help="skip the side measurements (decode-only rate, K7 BMP->IYUV roofline)")
     ap.add_argument("--breakdown-steps", type=int, default=5,
@@ -228,21 +232,36 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    # N>1: the batch's exchange step, every rank's compressed streams to rank 0
+    # (batch.ChunkedGather): chunks of --gather-chunk frames; a chunk's sizes
+    # are all-gathered when its launch groups are done and its streams sent
+    # while the following chunks compute
+    gat = None
+    if world > 1:
+        import batch
+        gat = batch.ChunkedGather(dist, world, rank, dev)
+    cg = max(1, args.gather_chunk // B)  # launch groups per chunk
+    ngr = (args.steps + B - 1) // B
     frames_ctx0 = 0  # frames in context 0's (event-stamped) launches
-    for j in range((args.steps + B - 1) // B):  # the last group takes the remainder
+    evs, c0 = [], 0
+    for j in range(ngr):  # the last group takes the remainder
         nb = min(B, args.steps - j * B)
         group(j, nb)
         frames_ctx0 += nb if j % nf == 0 else 0
+        if gat is not None:
+            ev = torch.cuda.Event()
+            ev.record(streams[j % nf])
+            evs.append(ev)
+            if len(evs) == cg or j == ngr - 1:
+                i1 = min((j + 1) * B, args.steps)
+                gat.add(list(range(c0, i1)), [d_pay[i] for i in range(c0, i1)], d_size[c0:i1], evs)
+                evs, c0 = [], i1
     for st in streams[1:]:
         streams[0].wait_stream(st)
     gathered = None
-    if world > 1:
-        # the batch's exchange step: every rank's compressed streams to rank 0
-        import batch
-        nframes = world * args.steps
-        got = batch.gather_streams(dist, [d_pay[i % nslot] for i in range(args.steps)],
-                                   d_size[:args.steps], nframes, world, rank, dev)
-        gathered = len(got) if got is not None else 0
+    if gat is not None:
+        got = gat.finish(args.steps)
+        gathered = sum(t is not None for t in got) if got is not None else 0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -72,3 +72,54 @@ def test_shard_is_round_robin():
     import batch
     assert batch.shard(10, 4, 1) == [1, 5, 9]
     assert sorted(sum((batch.shard(11, 3, r) for r in range(3)), [])) == list(range(11))
+
+
+def _chunk_worker(rank, world, port, n_local, chunk, q, out):
+    import sys
+    sys.path[:0] = [ROOT, PKG]
+    import torch
+    import torch.distributed as dist
+    import batch
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = batch.ChunkedGather(dist, world, rank, torch.device("cpu"))
+        for i0 in range(0, n_local, chunk):
+            local = list(range(i0, min(i0 + chunk, n_local)))
+            pays, sizes = [], []
+            for i in local:
+                p = O.compress(frame(rank + world * i), 64, 48, q)
+                pays.append(torch.frombuffer(bytearray(p + bytes(8)), dtype=torch.uint8))
+                sizes.append(len(p))
+            g.add(local, pays, torch.tensor(sizes, dtype=torch.int32))
+        got = g.finish(n_local)
+        if rank == 0:
+            out.put([bytes(t.numpy()) for t in got])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_local,chunk", [(2, 5, 2), (3, 4, 4), (2, 3, 1)])
+def test_chunked_gather_gloo(world, n_local, chunk):
+    """bench.py's overlapped gather (batch.ChunkedGather): chunks of every
+    rank's frames, sizes all-gathered per chunk, the previous chunk's packed
+    streams sent while the next is produced; rank 0 ends with every frame's
+    stream in global order."""
+    from oracle import oracle as O
+    q = (50, 60, 70)
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chunk_worker, args=(r, world, port, n_local, chunk, q, out))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = out.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(got) == world * n_local
+    for f in range(world * n_local):
+        assert got[f] == O.compress(frame(f), 64, 48, q), f

@@ -74,3 +74,106 @@ def run_batch(dist, frames, compress, n_frames, world, rank, device):
         sizes.append(s.reshape(1))
     size_t = torch.cat(sizes) if sizes else torch.zeros(0, dtype=torch.int32, device=device)
     return gather_streams(dist, payloads, size_t.to(torch.int32), n_frames, world, rank, device)
+
+
+class ChunkedGather:
+    """The gather of `gather_streams`, overlapped with the compression.
+
+    Every rank produces the same number of frames, in chunks (the bench: a
+    few launch groups).  For chunk c, `add` all-gathers the chunk's u32 sizes
+    on a side stream once the chunk's kernels are done (`ready` events), and
+    posts the point-to-point transfers of chunk c - 1, whose sizes are on the
+    host by then: one packed exact-size message per rank to rank 0, as in
+    gather_streams.  So the transfers of a chunk run while the next chunks
+    compute, and the host waits only for a size exchange that finished long
+    before.  Every rank issues the same collectives in the same order:
+    all_gather(0), all_gather(1), P2P(0), all_gather(2), P2P(1), ...
+
+    Local frame i of rank r is global frame r + world * i (shard()).  With
+    CPU tensors (gloo tests) there are no streams and every step is eager.
+    """
+
+    def __init__(self, dist, world, rank, device):
+        self.dist, self.world, self.rank, self.device = dist, world, rank, device
+        self.cuda = device.type == "cuda"
+        self.side = torch.cuda.Stream(device) if self.cuda else None
+        self.pending = []  # (local indices, payloads, host sizes [world][k], ready event)
+        self.works = []
+        self.keep = []
+        self.recv = []  # rank 0: (local indices, sizes [world][k], {rank: buffer})
+        self.received = 0
+
+    def _stream(self):
+        import contextlib
+        return torch.cuda.stream(self.side) if self.cuda else contextlib.nullcontext()
+
+    def add(self, local, payloads, sizes, ready=()):
+        """local: this chunk's local frame indices (the same list on every
+        rank); payloads: tensors holding the streams; sizes: int32 tensor of
+        their sizes; ready: CUDA events after which both are valid."""
+        k = len(local)
+        if self.cuda:
+            for e in ready:
+                self.side.wait_event(e)
+        with self._stream():
+            parts = [torch.empty(k, dtype=torch.int32, device=self.device) for _ in range(self.world)]
+            self.dist.all_gather(parts, sizes[:k].contiguous())
+            stacked = torch.stack(parts)
+            if self.cuda:
+                hs = torch.empty(stacked.shape, dtype=torch.int32, pin_memory=True)
+                hs.copy_(stacked, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            else:
+                hs, ev = stacked.clone(), None
+        self.pending.append((list(local), payloads, hs, ev))
+        if len(self.pending) > 1:
+            self._post(self.pending.pop(0))
+
+    def _post(self, item):
+        local, payloads, hs, ev = item
+        if ev is not None:
+            ev.synchronize()
+        hs = hs.tolist()
+        dist, rank = self.dist, self.rank
+        with self._stream():
+            if rank != 0:
+                total = sum(hs[rank])
+                if total > 0:
+                    packed = torch.cat([p[:n] for p, n in zip(payloads, hs[rank])])
+                    self.keep.append(packed)  # alive until finish() has waited
+                    self.works += dist.batch_isend_irecv([dist.P2POp(dist.isend, packed, 0)])
+                return
+            own = {i: p[:n] for i, p, n in zip(local, payloads, hs[0])}
+            bufs, ops = {}, []
+            for r in range(1, self.world):
+                total = sum(hs[r])
+                if total > 0:
+                    bufs[r] = torch.empty(total, dtype=torch.uint8, device=self.device)
+                    ops.append(dist.P2POp(dist.irecv, bufs[r], r))
+            if ops:
+                self.works += dist.batch_isend_irecv(ops)
+            self.recv.append((local, hs, bufs, own))
+
+    def finish(self, n_local):
+        """Posts what is left and waits for every transfer.  Rank 0 returns
+        the world * n_local streams in global frame order; None elsewhere."""
+        while self.pending:
+            self._post(self.pending.pop(0))
+        for w in self.works:
+            w.wait()
+        if self.rank != 0:
+            return None
+        out = [None] * (self.world * n_local)
+        for local, hs, bufs, own in self.recv:
+            for i, t in own.items():
+                out[self.world * i] = t
+            for r in range(1, self.world):
+                off = 0
+                for i, n in zip(local, hs[r]):
+                    b = bufs.get(r)
+                    out[r + self.world * i] = b[off:off + n] if n else torch.empty(0, dtype=torch.uint8,
+                                                                                   device=self.device)
+                    off += n
+        self.received = sum(t is not None for t in out)
+        return out
