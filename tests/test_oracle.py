@@ -207,3 +207,26 @@ def test_error_behaviour_vs_reference(oracle, ref, golden, gold):
         with pytest.raises(ref.RefError) as e2:
             ref.compress(bytes(ww * hh * 3 // 2), ww, hh, (50, 50, 50), "serial")
         assert str(e2.value) == MSGS[code]
+
+
+def test_tiled_8192_q50_known_answer(oracle, chef_big):
+    """tiled 8192x8192 input and q50 file hashes."""
+    import myyuv_file
+    f, raw = chef_big
+    t = synth.tiled_frame(raw, f.width, f.height, 8192, 8192).tobytes()
+    img = myyuv_file.YUVFile(width=8192, height=8192, data=t)
+    assert sha(img.dumps()) == "02843f4286c9b8a8d15272c7900283de3a8241725f2a42f805aea41ec46f5813"
+    pay = oracle.compress(t, 8192, 8192, (50, 50, 50))
+    assert len(pay) == 18269428
+    assert sha(img.compressed(b"222", pay).dumps()) == \
+        "ef0d2416b76466116558ea341c732123cc72657fe9969d54813327a3c97c236d"
+
+
+def test_noise_4k_known_answer(oracle):
+    import myyuv_file
+    n = synth.noise_frame(3840, 2160).tobytes()
+    img = myyuv_file.YUVFile(width=3840, height=2160, data=n)
+    assert sha(img.dumps()).startswith("9a69b129")
+    pay = oracle.compress(n, 3840, 2160, (50, 50, 50))
+    assert len(pay) == 9613725
+    assert sha(img.compressed(b"222", pay).dumps()).startswith("88ba856a")
