@@ -358,6 +358,14 @@ def main():
             a_iso = 3 * samples * B / (kernel_us["fdct_quant"] * 1e-6) / 1e9
             roof_iso = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
                         "avg_launch_us": kernel_us["fdct_quant"]}
+        # K6 (dequant + inverse DCT, 2 B in + 1 B out per sample) the same way
+        roof_k6 = None
+        if kernel_us.get("dequant_idct"):
+            a6 = 3 * samples * B / (kernel_us["dequant_idct"] * 1e-6) / 1e9
+            roof_k6 = {"kernel": "dequant_idct", "achieved": round(a6, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(a6 / HBM_PEAK_GBS, 4),
+                       "algorithmic_bytes_per_launch": 3 * samples * B,
+                       "avg_launch_us": kernel_us["dequant_idct"]}
         for k, us in kernel_us.items():
             log(f"kernel {k:16s} {us:9.2f} us/launch")
         cpu = None
@@ -374,7 +382,8 @@ def main():
                                    f"compress+decompress, HBM-resident, 1 frame/step/GPU",
                        "frame": f"{w}x{h}", "quality": q, "parallelism": f"frames sharded, dp{world}",
                        "launch_groups_in_flight": nf, "frames_per_launch": B, "payload_bytes": n0},
-            "roofline": roof, "roofline_isolated": roof_iso, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_isolated": roof_iso, "roofline_idct_isolated": roof_k6,
+            "cpu_baseline": cpu,
             "kernel_us": kernel_us or None,
             "side": side,
         }
