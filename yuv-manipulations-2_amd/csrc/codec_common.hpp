@@ -106,7 +106,10 @@ constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
 #endif
 constexpr uint32_t kWaveEncodeLimit = MYYUV_WAVE_LIMIT;
 constexpr uint32_t kWaveEncodeGrid = 8192;   // waves of k_huff_encode_wave (grid-stride)
-constexpr uint32_t kWideGrid = 1280;         // workgroups of k_huff_encode_wide: 5 per CU fit its LDS
+#ifndef MYYUV_WIDE_GRID
+#define MYYUV_WIDE_GRID 1280
+#endif
+constexpr uint32_t kWideGrid = MYYUV_WIDE_GRID;  // workgroups of k_huff_encode_wide: 5 per CU fit its LDS
 #ifndef MYYUV_K2_GROUP
 #define MYYUV_K2_GROUP 256
 #endif

@@ -386,20 +386,20 @@ __device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefRegs& 
     I.kc(p) = (w & 0x3FFFFu) | (len << 18);
   }
   STAMP(3);
-  // canonical order (length, symbol): insertion sort of slot ids into SH (u8)
+  // canonical order (length, symbol): slot p goes to SH (u8) position
+  // rank(p) = #{q : key(q) < key(p)} (keys are distinct).  The ranks are
+  // independent of one another, so the LDS reads pipeline, where an
+  // insertion sort is one chain of dependent round trips.
   for (int p = 0; p < n; p++) {
     const uint32_t wp = I.kc(p);
     const uint32_t kp = (((wp >> 18) & 15u) << 11) | (uint32_t)(nkey(wp) + 1024);
-    int j = p;
-    while (j > 0) {
-      const uint32_t q = I.sh8(j - 1);
+    uint32_t r = 0;
+    for (int q = 0; q < n; q++) {
       const uint32_t wq = I.kc(q);
       const uint32_t kq = (((wq >> 18) & 15u) << 11) | (uint32_t)(nkey(wq) + 1024);
-      if (kq <= kp) break;
-      I.sh8(j) = (uint8_t)q;
-      j--;
+      r += kq < kp ? 1u : 0u;
     }
-    I.sh8(j) = (uint8_t)p;
+    I.sh8((int)r) = (uint8_t)p;
   }
   STAMP(4);
 
