@@ -4,5 +4,5 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -3 gpurun_out/gpu_tests.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH_FAILED; tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
-bash tools/profile.sh r01k 20 && echo PROFILE_OK
+bash tools/profile.sh r01l 20 && echo PROFILE_OK
 timeout -k 10 120 python3 tools/kskip.py > gpurun_out/kskip.txt 2>&1 || true
