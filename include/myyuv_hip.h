@@ -134,6 +134,16 @@ int myyuv_gpu_bmp_to_iyuv(myyuv_hip_handle h, const uint8_t* bmp_data, int32_t w
 int myyuv_gpu_bmp_to_iyuv_device(myyuv_hip_handle h, const void* d_bmp_data, int32_t width,
                                  int32_t height, uint16_t bit_count, void* d_iyuv, void* stream);
 
+/* Host-buffer batch compress (many frames per call):
+ * `nframes` IYUV frames of one geometry back to back in `iyuv` (frame f at
+ * f*W*H*3/2) -> payload f at payloads + f*cap, its size in sizes[f].  One
+ * launch per kernel for the whole batch; every frame's bytes are those of
+ * myyuv_gpu_dct_compress.  MYYUV_E_CAPACITY when a payload exceeds `cap`
+ * (sizes[] still hold every size). */
+int myyuv_gpu_dct_compress_batch(myyuv_hip_handle h, const uint8_t* iyuv, uint32_t nframes,
+                                 uint32_t width, uint32_t height, const uint8_t quality[3],
+                                 uint8_t* payloads, uint32_t cap, uint32_t* sizes);
+
 /* Waits for `stream`, returns (and clears) the first device-side error since
  * the last call; *bad_block as above. */
 int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);

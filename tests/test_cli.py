@@ -133,3 +133,51 @@ def test_cli_to_yuv_matches_golden(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "BMP to YUV (IYUV) : " in r.stdout and r.stdout.endswith("Success!\n")
     assert out.read_bytes() == open(SMALL, "rb").read()
+
+
+@pytest.mark.gpu
+def test_cli_batch_compress_matches_per_file(tmp_path, golden, oracle):
+    """-batch-compress (many frames per invocation): two
+    copies of the small golden frame and a frame of another geometry; every
+    output equals the per-file result (the golden DCT-50 file for chef)."""
+    import numpy as np
+    import myyuv_file
+    a = tmp_path / "a.myyuv"
+    b = tmp_path / "b.myyuv"
+    c = tmp_path / "c.myyuv"
+    a.write_bytes(open(SMALL, "rb").read())
+    b.write_bytes(open(SMALL, "rb").read())
+    rng = np.random.default_rng(3)
+    raw = rng.integers(0, 256, 128 * 64 * 3 // 2).astype(np.uint8).tobytes()
+    myyuv_file.YUVFile(width=128, height=64, data=raw).dump(str(c))
+    out = tmp_path / "out"
+    out.mkdir()
+    r = run(CLI, "-batch-compress", "DCT", "50", "-o", str(out), str(a), str(b), str(c))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "(3 frames)" in r.stdout and r.stdout.endswith("Success!\n")
+    gold = open(C50, "rb").read()
+    assert (out / "a.myyuv").read_bytes() == gold
+    assert (out / "b.myyuv").read_bytes() == gold
+    one = tmp_path / "c1.myyuv"
+    assert run(CLI, str(c), "-compress", "DCT", "50", "-o", str(one)).returncode == 0
+    assert (out / "c.myyuv").read_bytes() == one.read_bytes()
+    # and back: -batch-decompress equals -decompress per file
+    dec = tmp_path / "dec"
+    dec.mkdir()
+    r = run(CLI, "-batch-decompress", "-o", str(dec), str(out / "a.myyuv"), str(out / "c.myyuv"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    one_d = tmp_path / "c1d.myyuv"
+    assert run(CLI, str(one), "-decompress", "-o", str(one_d)).returncode == 0
+    assert (dec / "c.myyuv").read_bytes() == one_d.read_bytes()
+    want = myyuv_file.YUVFile.load(gold)
+    assert myyuv_file.YUVFile.load(str(dec / "a.myyuv")).data == oracle.decompress(want.data, 992, 736, (50, 50, 50))
+
+
+@pytest.mark.gpu
+def test_python_compress_batch(codec, golden, chef_big):
+    f, raw = chef_big
+    small = golden("chef-with-trumpet.myyuv").data
+    pays = codec.compress_batch([raw, raw], f.width, f.height, (50, 50, 50))
+    one = codec.compress(raw, f.width, f.height, (50, 50, 50))
+    assert pays == [one, one]
+    assert codec.compress_batch([small], 992, 736, (50, 50, 50)) == [golden("chef-with-trumpet-DCT-50.myyuv").data]

@@ -9,6 +9,12 @@
 // (main.cpp:100-136):
 //   myyuv_cli in.bmp -info
 //   myyuv_cli in.bmp -to_yuv IYUV -o out.myyuv   (conversion on the GPU, K7)
+// and, beyond the reference CLI, many frames per invocation (SURVEY.md §8f
+// row 2; frames of one geometry share batched kernel launches):
+//   myyuv_cli -batch-compress DCT Q [Q [Q]] -o OUTDIR IN.myyuv...
+//   myyuv_cli -batch-decompress -o OUTDIR IN.myyuv...
+// each output is OUTDIR/<input file name>, byte-identical to the per-file
+// command's.
 #include <chrono>
 #include <cstring>
 #include <fstream>
@@ -37,6 +43,8 @@ void usage() {
             << "  myyuv_cli IMAGE.myyuv -decompress -o OUT.myyuv\n"
             << "  myyuv_cli IMAGE.bmp -info\n"
             << "  myyuv_cli IMAGE.bmp -to_yuv IYUV -o OUT.myyuv\n"
+            << "  myyuv_cli -batch-compress DCT Q [Q [Q]] -o OUTDIR IMAGE.myyuv...\n"
+            << "  myyuv_cli -batch-decompress -o OUTDIR IMAGE.myyuv...\n"
             << "\nYUV formats:\nIYUV\n\nCompression formats for YUV:\nDCT\n"
             << "\nExample:\n  myyuv_cli image.myyuv -compress DCT 50 -o image-DCT-50.myyuv\n";
 }
@@ -158,12 +166,71 @@ int run_bmp(const myyuv::BMP& bmp, size_t a, const std::vector<std::string>& arg
   return 1;
 }
 
+std::string base_name(const std::string& path) {
+  const size_t k = path.find_last_of('/');
+  return k == std::string::npos ? path : path.substr(k + 1);
+}
+
+// -batch-compress DCT Q [Q [Q]] -o OUTDIR FILES... / -batch-decompress -o OUTDIR FILES...
+int run_batch(const std::vector<std::string>& args) {
+  const bool comp = args[1] == "-batch-compress";
+  size_t a = 2;
+  std::vector<std::string> params;
+  if (comp) {
+    if (a >= args.size() || args[a] != "DCT")
+      throw std::runtime_error("Compression not registered: " + (a < args.size() ? args[a] : std::string()));
+    a++;
+    while (a < args.size() && args[a] != "-o") params.push_back(args[a++]);
+  }
+  if (a + 2 >= args.size() || args[a] != "-o") {
+    std::cout << "Invalid arguments. Expected -o OUTDIR followed by input files\n";
+    usage();
+    return 1;
+  }
+  const std::string outdir = args[a + 1];
+  std::vector<myyuv::YUV> in;
+  std::vector<std::string> names;
+  for (size_t i = a + 2; i < args.size(); i++) {
+    in.emplace_back(args[i]);
+    names.push_back(base_name(args[i]));
+  }
+  std::vector<myyuv::YUV> out;
+  const float ms = elapsed_ms([&] {
+    if (comp) {
+      uint8_t q[3];
+      if (params.empty()) throw std::runtime_error("Error. Too few compression parameters. Must be at least one.");
+      if (params.size() > 3)
+        throw std::runtime_error("Error. Too many compression parameters. Can't be more than 3 parameters.");
+      for (size_t i = 0; i < 3; i++) {
+        const int v = std::stoi(params[i < params.size() ? i : params.size() - 1]);
+        if (v < 1 || v > 100)
+          throw std::runtime_error("Error. Compression parameters for DCT must range between [1..100].");
+        q[i] = (uint8_t)v;
+      }
+      std::vector<const myyuv::YUV*> ptrs;
+      for (const auto& y : in) ptrs.push_back(&y);
+      out = myyuvDCT::compress_DCT_planar_batch(ptrs, {q[0], q[1], q[2]});
+    } else {
+      for (const auto& y : in) out.push_back(y.decompress());
+    }
+  });
+  std::cout << (comp ? "YUV DCT batch compression" : "YUV DCT batch decompression") << " (" << in.size()
+            << " frames) : " << ms << " ms\n";
+  for (size_t i = 0; i < out.size(); i++) out[i].dump(outdir + "/" + names[i]);
+  return 0;
+}
+
 int run(int argc, char* argv[]) {
   if (argc <= 2) {
     usage();
     return 0;
   }
   const std::vector<std::string> args(argv, argv + argc);
+  if (args[1] == "-batch-compress" || args[1] == "-batch-decompress") {
+    const int rc = run_batch(args);
+    if (rc == 0) std::cout << "Success!\n";
+    return rc;
+  }
   const std::string& path = args[1];
   char magic[2] = {0, 0};
   {

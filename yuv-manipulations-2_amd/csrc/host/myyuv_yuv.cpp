@@ -325,6 +325,52 @@ myyuv::YUV compress_DCT_planar(const myyuv::YUV& yuv, const std::array<uint8_t, 
   return res;
 }
 
+std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames,
+                                                  const std::array<uint8_t, 3>& params) {
+  using myyuv::YUV;
+  for (uint8_t q : params)
+    if (q < 1 || q > 100) throw std::runtime_error("Level of quality must be between 1 and 100");
+  for (const YUV* y : frames) {
+    if (y->getFormatGroup() != YUV::FormatGroup::PLANAR)
+      throw std::runtime_error("Error compressing: YUV must be planar");
+    if (y->getCompression() != YUV::Compressions::NONE)
+      throw std::runtime_error("Error compressing: can't compress uncompressed YUV");
+  }
+  std::vector<YUV> out(frames.size());
+  std::vector<bool> done(frames.size(), false);
+  constexpr size_t kMaxBatch = 16;  // frames per batched launch
+  for (size_t i = 0; i < frames.size(); i++) {
+    if (done[i]) continue;
+    const uint32_t w = frames[i]->header.width, h = frames[i]->header.height;
+    std::vector<size_t> group;  // this geometry, in input order
+    for (size_t j = i; j < frames.size() && group.size() < kMaxBatch; j++)
+      if (!done[j] && frames[j]->header.width == w && frames[j]->header.height == h) group.push_back(j);
+    const size_t fbytes = (size_t)w * h * 3 / 2;
+    const uint32_t cap = (myyuv_dct_payload_bound(w, h) + 3u) & ~3u;
+    std::vector<uint8_t> in(fbytes * group.size()), pay((size_t)cap * group.size());
+    std::vector<uint32_t> sizes(group.size());
+    for (size_t k = 0; k < group.size(); k++) std::memcpy(in.data() + k * fbytes, frames[group[k]]->data, fbytes);
+    const int rc = myyuv_gpu_dct_compress_batch(t_codec.get(), in.data(), (uint32_t)group.size(), w, h,
+                                                params.data(), pay.data(), cap, sizes.data());
+    if (rc) fail(rc);
+    for (size_t k = 0; k < group.size(); k++) {
+      const YUV& src = *frames[group[k]];
+      YUV& res = out[group[k]];
+      res.header = src.header;  // header rewrite as compress_DCT_planar (DCT.cpp:389-396)
+      res.header.compression = YUV::Compressions::DCT;
+      res.header.compression_params_size = 3;
+      res.header.compression_params_pos = sizeof(myyuv::YUVHeader);
+      res.header.data_pos = sizeof(myyuv::YUVHeader) + 3;
+      res.header.data_size = sizes[k];
+      res.compression_params = new uint8_t[3]{params[0], params[1], params[2]};
+      res.data = new uint8_t[sizes[k]];
+      std::memcpy(res.data, pay.data() + k * cap, sizes[k]);
+      done[group[k]] = true;
+    }
+  }
+  return out;
+}
+
 // decompress_DCT_planar (DCT.cpp:432-488): header rewrite (compression=0,
 // params 0/0, data at 64, data_size = image size), planes from the GPU.
 myyuv::YUV decompress_DCT_planar(const myyuv::YUV& yuv, const std::array<uint8_t, 3>& params) {

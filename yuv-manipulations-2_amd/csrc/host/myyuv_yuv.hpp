@@ -13,6 +13,7 @@
 #include <functional>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "myyuv_bmp.hpp"
 
@@ -105,4 +106,8 @@ namespace myyuvDCT {
 // myyuv_DCT/DCT.hpp:16,25 — same signatures, HIP implementation.
 myyuv::YUV compress_DCT_planar(const myyuv::YUV& yuv, const std::array<uint8_t, 3>& params);
 myyuv::YUV decompress_DCT_planar(const myyuv::YUV& yuv, const std::array<uint8_t, 3>& params);
+// Many frames per call: frames of one geometry share
+// one batched launch of every kernel; result i is compress_DCT_planar(*frames[i]).
+std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames,
+                                                  const std::array<uint8_t, 3>& params);
 }  // namespace myyuvDCT

@@ -161,6 +161,7 @@ struct myyuv_hip_ctx {
   hipStream_t stream = nullptr;
   DevBuf frame, coef, slots, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
   DevBuf bmp;   // staged BMP pixels (host-buffer BMP -> IYUV)
+  DevBuf bsizes;  // u32 payload sizes of a host-buffer batch
   DevBuf rmask; // per block: bit c = coefficient row c nonzero (K5 -> K6)
   DevBuf zq;    // 256 zero bytes: K6's source for rows the mask says are zero
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
@@ -517,7 +518,7 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff,  &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
-                    &c->bmp,   &c->rmask, &c->zq};
+                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -711,6 +712,47 @@ int myyuv_gpu_dct_compress(myyuv_hip_handle c, const uint8_t* iyuv, uint32_t w, 
   if (hipMemcpyAsync(payload, c->payload.p, size, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return MYYUV_E_HIP;
+  if (c->prof) drain_profile(c);
+  return 0;
+}
+
+int myyuv_gpu_dct_compress_batch(myyuv_hip_handle c, const uint8_t* iyuv, uint32_t nframes, uint32_t w,
+                                 uint32_t h, const uint8_t q[3], uint8_t* payloads, uint32_t cap,
+                                 uint32_t* sizes) {
+  if (!c || !iyuv || !payloads || !sizes || !q || nframes == 0) return MYYUV_E_ARG;
+  for (int p = 0; p < 3; p++)
+    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e || (e = set_batch(G, nframes))) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipStream_t s = c->stream;
+  const size_t fbytes = (size_t)w * h * 3 / 2;
+  const uint32_t dcap = (myyuv_dct_payload_bound(w, h) + 3) & ~3u;  // device slot per frame
+  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
+  if (c->frame.grow(fbytes * nframes) || c->payload.grow((size_t)dcap * nframes) ||
+      c->bsizes.grow((size_t)4 * nframes))
+    return MYYUV_E_HIP;
+  if (reset_err(c, s)) return MYYUV_E_HIP;
+  if (hipMemcpyAsync(c->frame.p, iyuv, fbytes * nframes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return MYYUV_E_HIP;
+  if ((e = launch_compress(c, G, c->frame.p, c->payload.p, dcap, c->bsizes.as<uint32_t>(), s))) return e;
+  if (hipMemcpyAsync(sizes, c->bsizes.p, (size_t)4 * nframes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return MYYUV_E_HIP;
+  int64_t bad = -1;
+  if ((e = read_err(c, s, &bad))) {
+    (void)reset_err(c, s);
+    return e;
+  }
+  for (uint32_t f = 0; f < nframes; f++)
+    if (sizes[f] > cap) return MYYUV_E_CAPACITY;
+  for (uint32_t f = 0; f < nframes; f++)
+    if (hipMemcpyAsync(payloads + (size_t)f * cap, static_cast<uint8_t*>(c->payload.p) + (size_t)f * dcap,
+                       sizes[f], hipMemcpyDeviceToHost, s) != hipSuccess)
+      return MYYUV_E_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return MYYUV_E_HIP;
   if (c->prof) drain_profile(c);
   return 0;
 }

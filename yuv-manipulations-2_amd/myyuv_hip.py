@@ -32,6 +32,7 @@ EXPORTS = [
     "myyuv_hip_profile", "myyuv_hip_profile_kernels", "myyuv_hip_kernel_stats", "myyuv_gpu_fdct_blocks",
     "myyuv_gpu_huff_encode_blocks", "myyuv_hip_reserve_batch", "myyuv_gpu_dct_compress_batch_device",
     "myyuv_gpu_dct_decompress_batch_device", "myyuv_gpu_bmp_to_iyuv", "myyuv_gpu_bmp_to_iyuv_device",
+    "myyuv_gpu_dct_compress_batch",
 ]
 
 _lib = None
@@ -99,6 +100,7 @@ def load():
     i32 = ctypes.c_int32
     L.myyuv_gpu_bmp_to_iyuv.argtypes = [vp, u8p, i32, i32, ctypes.c_uint16, u8p]
     L.myyuv_gpu_bmp_to_iyuv_device.argtypes = [vp, vp, i32, i32, ctypes.c_uint16, vp, vp]
+    L.myyuv_gpu_dct_compress_batch.argtypes = [vp, u8p, u32, u32, u32, u8p, u8p, u32, ctypes.POINTER(u32)]
     _lib = L
     return L
 
@@ -168,6 +170,19 @@ class Codec:
         if rc:
             raise CodecError(rc, bad.value)
         return out.tobytes()
+
+    def compress_batch(self, frames, w, h, q):
+        """Host-buffer batch: a list of IYUV frames of one geometry -> their
+        DCTYUV payloads (one launch per kernel for the batch)."""
+        n = len(frames)
+        src = np.ascontiguousarray(np.frombuffer(b"".join(bytes(f) for f in frames), np.uint8))
+        cap = (payload_bound(w, h) + 3) & ~3
+        out = np.empty(n * cap, np.uint8)
+        sizes = (ctypes.c_uint32 * n)()
+        rc = load().myyuv_gpu_dct_compress_batch(self._h, _u8(src), n, w, h, _u8(_q(q)), _u8(out), cap, sizes)
+        if rc:
+            raise CodecError(rc)
+        return [out[i * cap: i * cap + sizes[i]].tobytes() for i in range(n)]
 
     def bmp_to_iyuv(self, bmp_data, width, height, bit_count):
         """BMP::data (as stored; signed header width/height) -> IYUV bytes,
