@@ -4,7 +4,10 @@
 
 namespace myyuv_gpu {
 
-constexpr uint32_t kScanPerThread = 16;
+#ifndef MYYUV_SCAN_PER_THREAD
+#define MYYUV_SCAN_PER_THREAD 16
+#endif
+constexpr uint32_t kScanPerThread = MYYUV_SCAN_PER_THREAD;
 constexpr uint32_t kScanTile = 256 * kScanPerThread;
 
 // Where the u8 chunk-size bytes of each plane live in `src`.
