@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X DCT codec hot path (BASELINE.json `metric`).
 
-A step = one DCT compress + decompress round trip of one 4032x3008 IYUV frame
-(BASELINE.json configs[1]: chef-with-trumpet-big, q=50; its raw input is
-missing from the reference, so the frame is the decode of
-chef-with-trumpet-big-DCT-50.myyuv, sha-pinned), with the frame and the
-compressed stream resident in HBM: compress_device -> decompress_device on one
-stream.  value = megapixels (luma W*H) of all ranks' steps / max-over-ranks
-wall time of the K timed steps.
+A step = one DCT compress + decompress round trip of one batch of
+--inflight x --batch (default 3 x 4 = 12) 4032x3008 IYUV frames (BASELINE.json
+configs[1]: chef-with-trumpet-big, q=50; its raw input is missing from the
+reference, so the frame is the decode of chef-with-trumpet-big-DCT-50.myyuv,
+sha-pinned), with the frames and the compressed streams resident in HBM.
+value = megapixels (luma W*H) of all ranks' frames / max-over-ranks wall time
+of the K timed steps.  The frames are read from --input-frames (default 24)
+distinct copies in HBM (436 MB, more than the 256 MiB Infinity Cache), so
+every launch group reads its pixels from HBM, not from a cache-resident
+buffer.
 
 Batches and streams: a launch group of --batch frames (default 4) goes through
 the batch entry points (one launch per kernel for all of them: a 4K frame is
@@ -32,7 +35,10 @@ reference sources with OpenMP, kind "reference") — or the C restatement
 (oracle/, kind "port") when _ref is absent — timed on this box's host cores,
 rank 0 at N=1 only, on a bounded sample of the same workload.
 
-N>1 (torch.distributed.run, one rank per GPU): frames are sharded one per GPU
+N>1: `python bench.py --gpus N` with no WORLD_SIZE in the environment starts
+`torch.distributed.run --nproc-per-node N` as a child process before anything
+touches a GPU and exits with its status; under a launcher WORLD_SIZE must
+equal --gpus.  One rank per GPU: frames are sharded one per GPU
 (weak scaling); inside the timed region rank 0 gathers every rank's
 compressed streams over RCCL (batch.ChunkedGather: per chunk of frames the
 sizes are all-gathered, then one packed exact-size point-to-point message per
@@ -63,8 +69,9 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=480)
-    ap.add_argument("--warmup", type=int, default=48)
+    ap.add_argument("--steps", type=int, default=40,
+                    help="timed steps; a step is one batch of --inflight x --batch frames")
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--quality", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the cpu_baseline sample (0 disables it)")
@@ -83,8 +90,49 @@ def parse():
     ap.add_argument("--no-side", action="store_true",
                     help="skip the side measurements (decode-only rate, K7 BMP->IYUV roofline)")
     ap.add_argument("--breakdown-steps", type=int, default=5,
-                    help="untimed steps after the timed region with every kernel stamped")
+                    help="untimed launch groups after the timed region with every kernel stamped")
+    ap.add_argument("--input-frames", type=int, default=24,
+                    help="distinct HBM copies of the input frame the launch groups read in turn "
+                         "(24 x 18.2 MB = 436 MB: larger than the 256 MiB Infinity Cache)")
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help="only check the multi-rank launch: each rank joins a gloo group and "
+                         "rank 0 prints the world size and an all_reduce (no GPU)")
     return ap.parse_args()
+
+
+def maybe_launch(args):
+    """--gpus N > 1 without a launcher: start N ranks with torch.distributed.run
+    as a child process (nothing in this process has touched a GPU) and return
+    its exit status.  Under a launcher, WORLD_SIZE must equal --gpus."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench.py: launching", " ".join(cmd))
+    return subprocess.run(cmd).returncode
+
+
+def launch_selftest():
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([dist.get_rank() + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"world": dist.get_world_size(), "rank_sum": int(t.item())}), flush=True)
+    dist.destroy_process_group()
 
 
 def load_traffic():
@@ -105,22 +153,51 @@ def load_traffic():
         return None
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def usable_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count()
+
+
 def cpu_baseline(raw, w, h, q, seconds, threads):
-    """Reference OpenMP build (or the C restatement) on the host cores."""
-    ncpu = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    """Reference OpenMP build (or the C restatement) on the host cores, plus
+    the reference's serial build (its MYYUV_USE_OPENMP=OFF configuration,
+    myyuv_lib/CMakeLists.txt:28-31) as the 1-thread figure."""
+    nproc = usable_cpus()
+    ncpu = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc
     os.environ["OMP_NUM_THREADS"] = str(ncpu)
     mp = w * h / 1e6
+    host = {"cpu_model": cpu_model(), "cpus_visible": nproc}
     try:
         from oracle import ref as R
         if R.available("omp"):
             tc, td = R.bench(raw, w, h, (q, q, q), 1)
             iters = max(3, min(64, int(seconds / max(1e-3, (tc + td) / 1e3))))
             tc, td = R.bench(raw, w, h, (q, q, q), iters)
+            one = None
+            if R.available("serial"):
+                sc, sd = R.bench(raw, w, h, (q, q, q), 5, variant="serial")
+                one = {"value": round(mp / ((sc + sd) / 1e3), 2), "unit": "MP/s", "cores": 1,
+                       "sample": f"5 round trips (median) of the same frame, reference serial build "
+                                 f"(compress {sc:.1f} ms + decompress {sd:.1f} ms)"}
             return {"value": round(mp / ((tc + td) / 1e3), 2), "unit": "MP/s", "cores": ncpu,
                     "kind": "reference",
                     "sample": f"{iters} in-process compress+decompress round trips of the "
                               f"{w}x{h} q{q} frame (median; reference myyuv_lib -O3 OpenMP, "
-                              f"compress {tc:.1f} ms + decompress {td:.1f} ms)"}
+                              f"compress {tc:.1f} ms + decompress {td:.1f} ms)",
+                    "single_thread": one, **host}
     except Exception as e:  # fall back to the restatement
         log("cpu_baseline: reference build unavailable:", e)
     from oracle import oracle as O
@@ -140,12 +217,17 @@ def cpu_baseline(raw, w, h, q, seconds, threads):
     t = ts[len(ts) // 2]
     return {"value": round(mp / t, 2), "unit": "MP/s", "cores": ncpu, "kind": "port",
             "sample": f"{iters} compress+decompress round trips of the {w}x{h} q{q} frame "
-                      f"(median; C restatement -O2 OpenMP)"}
+                      f"(median; C restatement -O2 OpenMP)", **host}
 
 
 def main():
     args = parse()
-    import numpy as np
+    rc = maybe_launch(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.launch_selftest:
+        launch_selftest()
+        return
     import torch
     import myyuv_hip
     import myyuv_file
@@ -172,28 +254,40 @@ def main():
     mp = w * h / 1e6
     samples = w * h * 3 // 2
     cap = myyuv_hip.payload_bound(w, h)
-    # launch group j (frames j*B .. j*B+B-1) runs on codec context j % nf and
-    # its own stream (contexts own their scratch buffers, so groups in flight
-    # never share one)
+    # a step = nf launch groups of B frames; launch group j runs on codec
+    # context j % nf and its own stream (contexts own their scratch buffers,
+    # so groups in flight never share one)
     B = max(1, args.batch)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nf - 1)]
+    per_step = nf * B
+    frames = args.steps * per_step
+    # explicit streams: the null stream's handle is 0, which the C ABI reads as
+    # "the context's own stream" (the N>1 gather's events must see the launches)
+    streams = [torch.cuda.Stream(dev) for _ in range(nf)]
     sps = [st.cuda_stream for st in streams]
     cap = (cap + 3) & ~3  # payload slots of a batch are dword aligned
-    d_in = torch.frombuffer(bytearray(raw * B), dtype=torch.uint8).to(dev)
+    # distinct input copies (HBM-resident, more than the Infinity Cache holds);
+    # launch group j reads copies (j*B .. j*B+B-1) mod nin
+    nin = max(B, (max(args.input_frames, B) // B) * B)
+    d_in = torch.empty((nin, samples), dtype=torch.uint8, device=dev)
+    d_in[:] = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream(dev))
+    ingroups = nin // B
     d_out = torch.empty((nf, B * samples), dtype=torch.uint8, device=dev)
     # one payload slot per timed frame: the batch of compressed streams this
     # rank contributes (gathered to rank 0 at N>1)
-    ngroups = max(nf, (args.steps + B - 1) // B)
-    nslot = ngroups * B
+    nslot = max(frames, per_step * max(1, args.warmup))
     d_pay = torch.empty((nslot, cap), dtype=torch.uint8, device=dev)
     d_size = torch.zeros(nslot, dtype=torch.int32, device=dev)
     for c in codecs:
         c.reserve_batch(w, h, B)
+    slot_groups = nslot // B
 
     def group(j, nb=B):
         k = j % nf
-        f0 = (j % ngroups) * B
-        codecs[k].compress_batch_device(d_in.data_ptr(), nb, w, h, (q, q, q), d_pay[f0].data_ptr(), cap,
+        f0 = (j % slot_groups) * B
+        src = d_in[(j % ingroups) * B].data_ptr()
+        codecs[k].compress_batch_device(src, nb, w, h, (q, q, q), d_pay[f0].data_ptr(), cap,
                                         d_size[f0:f0 + nb].data_ptr(), sps[k])
         codecs[k].decompress_batch_device(d_pay[f0].data_ptr(), d_size[f0:f0 + nb].data_ptr(), cap, nb,
                                           w, h, (q, q, q), d_out[k].data_ptr(), sps[k])
@@ -204,7 +298,7 @@ def main():
             if rc:
                 raise SystemExit(f"codec error {rc} ({myyuv_hip.strerror(rc)}) at block {bad}")
 
-    for j in range(max(args.warmup // B, nf)):
+    for j in range(max(1, args.warmup) * nf):
         group(j)
     check_status()
     n0 = int(d_size[0].item())
@@ -212,7 +306,7 @@ def main():
     if q == 50 and hashlib.sha256(pay0).hexdigest() != BIG_RECOMPRESSED_SHA:
         raise SystemExit("compressed stream differs from the pinned reference bytes")
     host_rt = codec.decompress(pay0, w, h, (q, q, q))
-    for f in range(nf * B):
+    for f in range(per_step):
         nk = int(d_size[f].item())
         if bytes(d_pay[f, :nk].cpu().numpy()) != pay0:
             raise SystemExit(f"frame slot {f}: compressed stream differs from slot 0's")
@@ -221,11 +315,9 @@ def main():
             if bytes(d_out[k, b * samples:(b + 1) * samples].cpu().numpy()) != host_rt:
                 raise SystemExit(f"context {k} frame {b}: device round trip differs from the host-API decode")
 
-    # ---- timed region: only K1 (the roofline kernel) is event-stamped, so the
-    # other launches carry no profiling cost
-    # K1's launches on context 0 (one launch group in nf, spread evenly over
-    # the timed region) carry the HIP events: stamping every context's
-    # launches costs ~5 % of throughput (event records on all queues)
+    # ---- timed region: only K1 (the roofline kernel) is event-stamped, on
+    # context 0's launches (one launch group in nf, spread evenly over the
+    # region): stamping every context's launches costs ~5 % of throughput
     if not args.no_kernel_events:
         codecs[0].profile(True, kernels=["fdct_quant"])
     if world > 1:
@@ -241,32 +333,30 @@ def main():
         import batch
         gat = batch.ChunkedGather(dist, world, rank, dev)
     cg = max(1, args.gather_chunk // B)  # launch groups per chunk
-    ngr = (args.steps + B - 1) // B
-    frames_ctx0 = 0  # frames in context 0's (event-stamped) launches
+    ngr = args.steps * nf
     evs, c0 = [], 0
-    for j in range(ngr):  # the last group takes the remainder
-        nb = min(B, args.steps - j * B)
-        group(j, nb)
-        frames_ctx0 += nb if j % nf == 0 else 0
+    for j in range(ngr):
+        group(j)
         if gat is not None:
             ev = torch.cuda.Event()
             ev.record(streams[j % nf])
             evs.append(ev)
             if len(evs) == cg or j == ngr - 1:
-                i1 = min((j + 1) * B, args.steps)
+                i1 = (j + 1) * B
                 gat.add(list(range(c0, i1)), [d_pay[i] for i in range(c0, i1)], d_size[c0:i1], evs)
                 evs, c0 = [], i1
-    for st in streams[1:]:
-        streams[0].wait_stream(st)
+    for st in streams:
+        torch.cuda.current_stream(dev).wait_stream(st)
     gathered = None
     if gat is not None:
-        got = gat.finish(args.steps)
+        got = gat.finish(frames)
         gathered = sum(t is not None for t in got) if got is not None else 0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
     check_status()
+    frames_ctx0 = args.steps * B  # frames in context 0's (event-stamped) launches
     stats = {}
     if not args.no_kernel_events:
         for kname, (kms, kn) in codecs[0].kernel_stats().items():
@@ -278,7 +368,7 @@ def main():
     if args.breakdown_steps > 0:
         codec.profile(True)
         for i in range(args.breakdown_steps):
-            group(0)
+            group(i * nf)
         codec.sync_status(sps[0])
         breakdown = codec.kernel_stats()
         codec.profile(False)
@@ -288,14 +378,13 @@ def main():
         side = {}
         # decode-only batched rate: the same launch groups, decompress only,
         # from the streams the timed region left in HBM
-        full = max(1, args.steps // B)  # groups whose B slots all hold a stream
 
         def dgroup(j):
             k = j % nf
-            f0 = (j % full) * B
+            f0 = (j % (frames // B)) * B
             codecs[k].decompress_batch_device(d_pay[f0].data_ptr(), d_size[f0:f0 + B].data_ptr(), cap, B,
                                               w, h, (q, q, q), d_out[k].data_ptr(), sps[k])
-        nd = max(nf, args.steps // B)
+        nd = ngr
         for j in range(nf):
             dgroup(j)
         torch.cuda.synchronize(dev)
@@ -335,11 +424,11 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
         if rank == 0:
-            assert gathered == world * args.steps, gathered
+            assert gathered == world * frames, gathered
 
     if rank == 0:
         ms_step = t / args.steps * 1e3
-        value = world * args.steps * mp / t
+        value = world * frames * mp / t
         k1_ms, k1_n = stats.get("fdct_quant", (0.0, 0))
         roof = None
         if k1_n:
@@ -377,11 +466,12 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8/int16 (fp32 transform)",
             "data": "chef-with-trumpet-big-DCT-50.myyuv decoded (4032x3008 IYUV, sha-pinned); "
-                    "stand-in for the missing raw 4K",
+                    f"stand-in for the missing raw 4K; {nin} distinct HBM copies",
             "config": {"workload": f"chef-with-trumpet-big 4032x3008 IYUV DCT q={q} "
-                                   f"compress+decompress, HBM-resident, 1 frame/step/GPU",
+                                   f"compress+decompress, HBM-resident, {per_step} frames/step/GPU",
                        "frame": f"{w}x{h}", "quality": q, "parallelism": f"frames sharded, dp{world}",
-                       "launch_groups_in_flight": nf, "frames_per_launch": B, "payload_bytes": n0},
+                       "frames_per_step": per_step, "launch_groups_in_flight": nf,
+                       "frames_per_launch": B, "input_copies": nin, "payload_bytes": n0},
             "roofline": roof, "roofline_isolated": roof_iso, "roofline_idct_isolated": roof_k6,
             "cpu_baseline": cpu,
             "kernel_us": kernel_us or None,

@@ -57,7 +57,11 @@ typedef struct myyuv_hip_ctx* myyuv_hip_handle;
 /* Context: one per (host thread, device).  Owns a HIP stream, the per-call
  * workspace (grown on demand, never freed inside a call) and pinned staging
  * buffers for the host-buffer entry points.  Reentrant across contexts, as the
- * reference is (SURVEY.md §8b "Threading"). */
+ * reference is (SURVEY.md §8b "Threading").  Calls through ONE context share
+ * its workspace, so they run in call order even on different streams: a call
+ * on a stream other than the previous call's makes its stream wait for the
+ * previous call's work (an event recorded at the end of every call).  For
+ * concurrency, use one context per stream. */
 int myyuv_hip_create(int device, myyuv_hip_handle* out);
 void myyuv_hip_destroy(myyuv_hip_handle h);
 const char* myyuv_hip_strerror(int code);

@@ -181,3 +181,25 @@ def test_python_compress_batch(codec, golden, chef_big):
     one = codec.compress(raw, f.width, f.height, (50, 50, 50))
     assert pays == [one, one]
     assert codec.compress_batch([small], 992, 736, (50, 50, 50)) == [golden("chef-with-trumpet-DCT-50.myyuv").data]
+
+
+def test_batch_rejects_duplicate_output_names(tmp_path):
+    """Batch outputs are OUTDIR/<input file name>: two inputs with the same
+    file name from different directories are refused before any work."""
+    d1, d2, out = tmp_path / "a", tmp_path / "b", tmp_path / "out"
+    for d in (d1, d2, out):
+        d.mkdir()
+    data = open(SMALL, "rb").read()
+    (d1 / "f.myyuv").write_bytes(data)
+    (d2 / "f.myyuv").write_bytes(data)
+    r = run(CLI, "-batch-compress", "DCT", "50", "-o", str(out), str(d1 / "f.myyuv"), str(d2 / "f.myyuv"))
+    assert r.returncode != 0
+    assert "share the file name f.myyuv" in r.stderr
+    assert not os.listdir(out)
+
+
+@pytest.mark.gpu
+def test_python_compress_batch_checks_frame_sizes(codec):
+    raw = open(SMALL, "rb").read()[64:]
+    with pytest.raises(ValueError, match="frame 1"):
+        codec.compress_batch([raw, raw[:-1]], 992, 736, (50, 50, 50))

@@ -123,3 +123,35 @@ def test_chunked_gather_gloo(world, n_local, chunk):
     assert len(got) == world * n_local
     for f in range(world * n_local):
         assert got[f] == O.compress(frame(f), 64, 48, q), f
+
+
+def _bench_env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["HIP_VISIBLE_DEVICES"] = ""  # nothing in the launch check may touch a GPU
+    return env
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` with no launcher in the environment starts two ranks
+    (torch.distributed.run as a child process); --launch-selftest makes each
+    rank join a gloo group, and rank 0 reports world 2 and 1 + 2 = 3."""
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-selftest"],
+                       capture_output=True, text=True, timeout=240, env=_bench_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    assert json.loads(line) == {"world": 2, "rank_sum": 3}
+
+
+def test_bench_rejects_rank_count_mismatch():
+    import subprocess
+    import sys
+    env = _bench_env()
+    env.update(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-selftest"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode != 0
+    assert "--gpus 2 but the launcher started 3 ranks" in r.stderr

@@ -191,9 +191,14 @@ int run_batch(const std::vector<std::string>& args) {
   std::vector<myyuv::YUV> in;
   std::vector<std::string> names;
   for (size_t i = a + 2; i < args.size(); i++) {
-    in.emplace_back(args[i]);
     names.push_back(base_name(args[i]));
+    // outputs are OUTDIR/<input file name>: two inputs with one name would
+    // overwrite each other
+    for (size_t j = 0; j + 1 < names.size(); j++)
+      if (names[j] == names.back())
+        throw std::runtime_error("Error. Two batch inputs share the file name " + names.back());
   }
+  for (size_t i = a + 2; i < args.size(); i++) in.emplace_back(args[i]);
   std::vector<myyuv::YUV> out;
   const float ms = elapsed_ms([&] {
     if (comp) {

@@ -159,6 +159,12 @@ int set_batch(FrameGeom& G, uint32_t nf) {
 struct myyuv_hip_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // One context's scratch buffers (coef, slots, sizes, scan status words ...)
+  // serve one call at a time: every entry point records `done` on its stream
+  // and a call on another stream first waits for it (StreamOrder), so calls
+  // on different streams through one context run in call order.
+  hipEvent_t done = nullptr;
+  hipStream_t last_stream = nullptr;
   DevBuf frame, coef, slots, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
   DevBuf bmp;   // staged BMP pixels (host-buffer BMP -> IYUV)
   DevBuf bsizes;  // u32 payload sizes of a host-buffer batch
@@ -197,6 +203,19 @@ struct DeviceGuard {
   ~DeviceGuard() {
     int cur = -1;
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Orders a call on stream `s` after the context's previous call (see
+// myyuv_hip_ctx::done); the record at scope exit publishes this call's work.
+struct StreamOrder {
+  myyuv_hip_ctx* c;
+  hipStream_t s;
+  StreamOrder(myyuv_hip_ctx* ctx, hipStream_t st) : c(ctx), s(st) {
+    if (c->last_stream && c->last_stream != s) (void)hipStreamWaitEvent(s, c->done, 0);
+  }
+  ~StreamOrder() {
+    if (hipEventRecord(c->done, s) == hipSuccess) c->last_stream = s;
   }
 };
 
@@ -490,6 +509,11 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
     delete c;
     return MYYUV_E_HIP;
   }
+  if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return MYYUV_E_HIP;
+  }
   {
     int cus = 0, n1 = 0, n6 = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
@@ -502,6 +526,7 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
   }
   if (c->err.grow(8) || c->psize.grow(4) || c->desc.grow(sizeof(StreamDesc)) ||
       hipMemset(c->err.p, 0xFF, 8) != hipSuccess) {
+    (void)hipEventDestroy(c->done);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return MYYUV_E_HIP;
@@ -514,8 +539,10 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   if (!c) return;
   DeviceGuard g(c->device);
   (void)hipStreamSynchronize(c->stream);
+  if (c->last_stream) (void)hipEventSynchronize(c->done);
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(c->done);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff,  &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
                     &c->bmp,   &c->rmask, &c->zq, &c->bsizes};
@@ -548,6 +575,7 @@ int myyuv_gpu_dct_compress_batch_device(myyuv_hip_handle c, const void* d_in, ui
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  StreamOrder so(c, s);
   if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
   return launch_compress(c, G, d_in, d_out, cap, d_sizes, s);
 }
@@ -566,6 +594,7 @@ int myyuv_gpu_dct_decompress_batch_device(myyuv_hip_handle c, const void* d_in, 
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  StreamOrder so(c, s);
   if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
   return launch_decompress(c, G, d_in, d_sizes, cap, d_out, s);
 }
@@ -641,6 +670,7 @@ int myyuv_gpu_bmp_to_iyuv_device(myyuv_hip_handle c, const void* d_bmp, int32_t 
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  StreamOrder so(c, s);
   return launch_bmp(c, d_bmp, W, H, orient, bit_count, d_iyuv, s);
 }
 
@@ -653,6 +683,7 @@ int myyuv_gpu_bmp_to_iyuv(myyuv_hip_handle c, const uint8_t* bmp_data, int32_t w
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
+  StreamOrder so(c, s);
   const size_t in_bytes = (size_t)W * H * (bit_count / 8), out_bytes = (size_t)W * H * 3 / 2;
   if (in_bytes == 0) return 0;
   if (c->bmp.grow(in_bytes) || c->frame.grow(out_bytes)) return MYYUV_E_HIP;
@@ -671,6 +702,7 @@ int myyuv_hip_sync_status(myyuv_hip_handle c, void* stream, int64_t* bad_block) 
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  StreamOrder so(c, s);
   int code = read_err(c, s, bad_block);
   if (reset_err(c, s) || hipStreamSynchronize(s) != hipSuccess) return MYYUV_E_HIP;
   if (c->prof) drain_profile(c);
@@ -689,6 +721,7 @@ int myyuv_gpu_dct_compress(myyuv_hip_handle c, const uint8_t* iyuv, uint32_t w, 
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
+  StreamOrder so(c, s);
   const size_t fbytes = (size_t)w * h * 3 / 2;
   const uint32_t bound = myyuv_dct_payload_bound(w, h);
   if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
@@ -728,6 +761,7 @@ int myyuv_gpu_dct_compress_batch(myyuv_hip_handle c, const uint8_t* iyuv, uint32
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
+  StreamOrder so(c, s);
   const size_t fbytes = (size_t)w * h * 3 / 2;
   const uint32_t dcap = (myyuv_dct_payload_bound(w, h) + 3) & ~3u;  // device slot per frame
   if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
@@ -774,6 +808,7 @@ int myyuv_gpu_dct_decompress(myyuv_hip_handle c, const uint8_t* payload, uint32_
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
+  StreamOrder so(c, s);
   const uint32_t cap = (size + 3) & ~3u;
   const size_t fbytes = (size_t)w * h * 3 / 2;
   if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
@@ -908,6 +943,7 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
+  StreamOrder so(c, s);
   // one plane of width 8 (one block per block-row); planes 1, 2 empty
   FrameGeom G;
   std::memset(&G, 0, sizeof(G));
@@ -965,6 +1001,7 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   hipStream_t s = c->stream;
+  StreamOrder so(c, s);
   FrameGeom G;
   std::memset(&G, 0, sizeof(G));
   G.cum[1] = G.cum[2] = G.cum[3] = nblocks;

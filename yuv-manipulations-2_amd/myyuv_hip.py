@@ -175,6 +175,10 @@ class Codec:
         """Host-buffer batch: a list of IYUV frames of one geometry -> their
         DCTYUV payloads (one launch per kernel for the batch)."""
         n = len(frames)
+        fb = w * h * 3 // 2
+        for i, f in enumerate(frames):
+            if len(memoryview(f).cast("B")) != fb:
+                raise ValueError(f"frame {i}: {len(memoryview(f).cast('B'))} bytes, a {w}x{h} IYUV frame has {fb}")
         src = np.ascontiguousarray(np.frombuffer(b"".join(bytes(f) for f in frames), np.uint8))
         cap = (payload_bound(w, h) + 3) & ~3
         out = np.empty(n * cap, np.uint8)
