@@ -46,8 +46,8 @@ def run(exe, nat, mode):
 
 
 def check(exe, oracle, nat):
-    """Every mode: encode_block_r<4>, encode_block_r<8>, and the kernel's
-    class dispatch ("auto", which adds encode_block_single).  A block is
+    """Every mode: build_r<4>, build_r<8> (each + emit_chunk), and the
+    kernel's class dispatch ("auto", which adds build_single).  A block is
     declined exactly when it has more distinct symbols than the CAP."""
     nat = np.asarray(nat, np.int16).reshape(-1, 64)
     n_ok = 0
@@ -99,3 +99,30 @@ def test_r8_golden_frame_blocks(harness, oracle, golden):
         Q = oracle.qtable(q, 0)
         nat = np.stack([oracle.fdct_block(y[i], Q) for i in pick])
         assert check(harness, oracle, nat) > 2000
+
+
+def test_dense_run_matches_concatenated_chunks(harness, oracle):
+    """K2's tile packing (DenseWriter): the accepted blocks' chunks back to
+    back in block order, every dword stored by the block owning its first
+    byte and completed with the next chunk's header; the run must equal the
+    concatenation of the oracle's chunks (declined blocks leave no gap)."""
+    rng = np.random.default_rng(11)
+    nat = np.zeros((256, 64), np.int16)
+    for x in nat:
+        m = rng.integers(1, 65)
+        nd = rng.integers(1, 12)
+        vals = rng.integers(-6, 7, nd)
+        keep = rng.random(64) < rng.random()
+        x[ZZ[:m]] = np.where(keep[:m], rng.choice(vals, m), 0)
+    out = subprocess.run([harness, "dense"], input=struct.pack("<I", len(nat)) + nat.tobytes(),
+                         capture_output=True, check=True).stdout
+    total = struct.unpack("<I", out[:4])[0]
+    want = b""
+    for x in nat:
+        msg = x[ZZ]
+        nz = np.nonzero(msg)[0]
+        m = nz[-1] + 1 if len(nz) else 1
+        if len(set(msg[:m].tolist())) <= 8:
+            want += bytes(oracle.huff_encode_block(x))
+    assert total == len(want)
+    assert out[4:] == want

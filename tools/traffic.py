@@ -7,7 +7,10 @@ Reads gpurun_out/prof_<tag>/{trace,fetch,write}/run_*.csv and writes
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
 coalesced stream, so read bytes = 2 * FETCH_SIZE * 1024 for kernels whose
-reads are 16-B-per-lane streams, write bytes = WRITE_SIZE * 1024.
+reads are 16-B-per-lane streams, write bytes = WRITE_SIZE * 1024.  K1's 8-B
+row loads / 16-B quad stores and K6's quad loads / 8-B row stores have their
+own factors, measured on known byte counts with the same addressing
+(tools/ubench/calib.hip -> profiles/<tag>_calib.json, newest one used).
 """
 import collections
 import csv
@@ -27,6 +30,20 @@ def per_kernel(path):
     return {k: sum(v) / len(v) for k, v in d.items()}
 
 
+# codec kernel -> (read shape, write shape) of tools/ubench/calib.hip
+CALIB_SHAPES = {"fdct_quant": ("k1_read", "k1_write"), "dequant_idct": ("k6_read", "k6_write")}
+
+
+def calib_factors():
+    pdir = os.path.join(ROOT, "profiles")
+    names = sorted(n for n in os.listdir(pdir) if n.endswith("_calib.json"))
+    if not names:
+        return {}, None
+    with open(os.path.join(pdir, names[-1])) as f:
+        d = json.load(f)
+    return {k: v["factor"] for k, v in d.items() if isinstance(v, dict)}, names[-1]
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
@@ -39,15 +56,20 @@ def main(tag):
             durations[r["Name"].split("(")[0].replace("myyuv_gpu::k_", "")] = float(r["AverageNs"])
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"))
+    cf, cname = calib_factors()
     out = {"_note": "bytes per launch; read = 2 x FETCH_SIZE (gfx950 wide-stream correction), "
-                    "write = WRITE_SIZE; both KiB x 1024; avg_ns from the kernel-trace pass"}
+                    "write = WRITE_SIZE; both KiB x 1024; fdct_quant / dequant_idct use the factors "
+                    f"measured for their own access shapes ({cname}); avg_ns from the kernel-trace pass"}
     for k in sorted(set(fetch) | set(write)):
         if k.startswith("__amd") or "at::native" in k:
             continue
-        rd = 2.0 * fetch.get(k, 0.0) * 1024
-        wr = write.get(k, 0.0) * 1024
+        rs, ws = CALIB_SHAPES.get(k, (None, None))
+        rf, wf = cf.get(rs, 2.0), cf.get(ws, 1.0)
+        rd = rf * fetch.get(k, 0.0) * 1024
+        wr = wf * write.get(k, 0.0) * 1024
         out[k] = {"fetch_kib": round(fetch.get(k, 0.0), 1), "write_kib": round(write.get(k, 0.0), 1),
                   "hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
+                  "read_factor": rf, "write_factor": wf,
                   "hbm_bytes_per_launch": int(rd + wr), "avg_ns": durations.get(k)}
     with open(os.path.join(dst, f"{tag}_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -59,6 +59,10 @@ struct FrameGeom {
   uint32_t nframes;
   uint32_t fbytes;        // W * H * 3 / 2
   uint64_t umag;          // ceil(2^64 / ucum[3]) (0 for 1 unit): batch unit -> frame
+  // K2 / K4 tiles: kK2Group consecutive blocks of one plane (the last tile of
+  // a plane may be shorter), cumulative per plane; tile t of frame f is
+  // batch tile f * tcum[3] + t
+  uint32_t tcum[4];
 };
 
 // floor(x / d) for a 32-bit x from m = ceil(2^64 / d) (m = 0 for d = 1): the
@@ -116,6 +120,38 @@ constexpr uint32_t kWideGrid = MYYUV_WIDE_GRID;  // workgroups of k_huff_encode_
 constexpr uint32_t kK2Group = MYYUV_K2_GROUP;  // blocks per workgroup of k_huff_encode
 __host__ __device__ __forceinline__ uint32_t coef_quad(uint32_t g, uint32_t c) {
   return ((g >> 6) * 8u + c) * 64u + (g & 63u);
+}
+
+// K2 -> K4 hand-off, per batch tile T:
+//   stage:  T * kTileCap bytes, one kWaveRun-byte region per K2 wave: the
+//           chunks of the wave's blocks with at most 8 distinct symbols, back
+//           to back in the wave's (class-sorted) order (a "dense run");
+//   srcoff: u16 per block: the chunk's byte offset in its tile's stage
+//           region, kSrcOverflow for a block with more symbols, whose chunk
+//           the overflow passes write to oslots at g * kMaxChunk;
+//   tinfo:  kTInfoWords u32 per tile: [0] overflow chunk bytes (the overflow
+//           passes add to it), [1 .. 4] dense-run bytes of K2's waves 0..3,
+//           [8] the tile's exclusive prefix in its frame's content
+//           (k_tile_scan).
+constexpr uint32_t kTileCap = kK2Group * kMaxChunk;
+constexpr uint32_t kWaveRun = kWave * kMaxChunk;
+constexpr uint32_t kTInfoWords = 16;
+constexpr uint32_t kTInfoPrefix = 8;
+constexpr uint16_t kSrcOverflow = 0xFFFF;
+
+// Plane, first block (frame-local) and block count of tile t of a frame.
+__host__ __device__ __forceinline__ int tile_plane(const FrameGeom& G, uint32_t t) {
+  return t >= G.tcum[1] ? (t >= G.tcum[2] ? 2 : 1) : 0;
+}
+__host__ __device__ __forceinline__ uint32_t tile_first(const FrameGeom& G, int p, uint32_t t) {
+  return G.cum[p] + (t - G.tcum[p]) * kK2Group;
+}
+// Batch tile of batch-global block g.
+__host__ __device__ __forceinline__ uint32_t tile_of_block(const FrameGeom& G, uint32_t g) {
+  const uint32_t f = G.nframes > 1 ? g / G.cum[3] : 0u;
+  const uint32_t l = g - f * G.cum[3];
+  const int p = l >= G.cum[1] ? (l >= G.cum[2] ? 2 : 1) : 0;
+  return f * G.tcum[3] + G.tcum[p] + (l - G.cum[p]) / kK2Group;
 }
 
 }  // namespace myyuv_gpu

@@ -63,9 +63,10 @@ MYYUV_HD uint32_t bucket_of(int v, const Phase& P) {
   return t - q * P.nb;
 }
 
-// LSB-first bit writer into the block's output slot.
+// LSB-first bit writer into a block's contiguous 160-B overflow slot
+// (k_huff_encode_wide / _wave: blocks with more than 8 distinct symbols).
 struct BitWriter {
-  uint32_t* out;  // &slot word 0 of this block; words kWave apart
+  uint32_t* out;  // slot word 0 of this block
   uint64_t acc = 0;
   int nacc = 0;
   int widx = 0;
@@ -73,7 +74,7 @@ struct BitWriter {
     acc |= (uint64_t)v << nacc;
     nacc += n;
     if (nacc >= 32) {
-      out[widx * kWave] = (uint32_t)acc;
+      out[widx] = (uint32_t)acc;
       widx++;
       acc >>= 32;
       nacc -= 32;
@@ -81,7 +82,51 @@ struct BitWriter {
   }
   MYYUV_HD void align_byte() { nacc = (nacc + 7) & ~7; }
   MYYUV_HD void flush() {
-    if (nacc > 0) out[widx * kWave] = (uint32_t)acc;
+    if (nacc > 0) out[widx] = (uint32_t)acc;
+  }
+};
+
+// LSB-first bit writer for K2's dense tile run: a workgroup's chunks are
+// packed back to back in block order (byte offsets from an in-tile scan), and
+// every dword is stored by exactly one lane — the block that owns the dword's
+// first byte.  A chunk therefore skips its first dword when it starts
+// mid-dword (the previous block stores it) and completes its last dword with
+// the first bytes of the next chunk in the run.  Those can only be the next
+// chunk's 3-byte header (u16 nbits, u8 table_bytes: a chunk is >= 7 bytes),
+// which every block knows before anything is emitted.  No atomics, no
+// read-modify-write, no shared words.
+struct DenseWriter {
+  uint32_t* base;  // the tile run, dword aligned
+  uint32_t widx;   // dword being filled
+  uint64_t acc;
+  int nacc;
+  bool skip;       // the dword being filled belongs to the previous chunk
+  MYYUV_HD void init(uint32_t* run, uint32_t off) {
+    base = run;
+    widx = off >> 2;
+    nacc = (int)(off & 3u) * 8;
+    acc = 0;
+    skip = (off & 3u) != 0;
+  }
+  MYYUV_HD void put(uint32_t v, int n) {
+    acc |= (uint64_t)v << nacc;
+    nacc += n;
+    if (nacc >= 32) {
+      if (!skip) base[widx] = (uint32_t)acc;
+      skip = false;
+      widx++;
+      acc >>= 32;
+      nacc -= 32;
+    }
+  }
+  MYYUV_HD void align_byte() { nacc = (nacc + 7) & ~7; }
+  // after the last byte: next = the next chunk's header | 1 << 31 (0: none)
+  MYYUV_HD void finish(uint32_t next) {
+    align_byte();
+    if (nacc > 0) {
+      if (next >> 31) acc |= (uint64_t)(next & 0xFFFFFFu) << nacc;
+      base[widx] = (uint32_t)acc;  // (a chunk spans > 4 bytes: never the skipped dword)
+    }
   }
 };
 
@@ -271,10 +316,22 @@ MYYUV_HD uint32_t f16(const uint32_t (&a)[CAP / 2], uint32_t i) {
 
 }  // namespace rr
 
+// What emit_chunk needs of a block whose code was built (build_r /
+// build_single), held in registers across k_huff_encode's in-tile scan of the
+// chunk sizes: <= 8 symbols.
+struct EncState {
+  uint32_t hdr;      // the chunk's first 3 bytes: u16 nbits | u8 table_bytes << 16
+  uint32_t size;     // chunk bytes: 3 + table_bytes + ceil(nbits / 8)
+  uint32_t n;        // distinct symbols
+  uint32_t msz;      // message length (positions)
+  uint64_t lcount;   // per code length L: symbols of that length (byte L - 1)
+  uint32_t TK[4];    // table in canonical order: entry r = key & 0x7FF | len << 11 (16-bit fields)
+  uint32_t CT[4];    // per slot k: len << 8 | bit-reversed code (16-bit fields)
+  SlotIds<8> ids;    // per position: slot of its symbol
+};
+
 template <int CAP>
-MYYUV_HD bool encode_block_r(const CoefRegs& R, int msz, int wave_msz,
-                                                uint32_t* __restrict__ slot,
-                                                uint8_t* __restrict__ size_out) {
+MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
   using namespace rr;
   static_assert(CAP == 4 || CAP == 8, "CAP");
   constexpr int NP = CAP / 2;
@@ -450,25 +507,48 @@ MYYUV_HD bool encode_block_r(const CoefRegs& R, int msz, int wave_msz,
     CT[k >> 1] |= ((len[k] << 8) | (rcode & 0xFFu)) << (16 * (k & 1));
   }
 
-  R8_STAMP(4);
-  // ---------------- 5. chunk bytes (Huffman.cpp:279-326) ----------------
-  BitWriter bw;
-  bw.out = slot;
-  bw.put(nbits, 16);
-  bw.put(table_bytes, 8);
-  // table: canonical order; a group header where the length changes
-  uint32_t curlen = 0;
+  // the table in canonical order for the emitter
+  uint32_t TK[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int r = 0; r < CAP; r++) {
-    if ((uint32_t)r < n) {
-      uint32_t kl = 0;  // key & 0x7FF | len << 11 of the symbol ranked r
+    uint32_t kl = 0;  // key & 0x7FF | len << 11 of the symbol ranked r
 #pragma unroll
-      for (int k = 0; k < CAP; k++)
-        kl = crank[k] == (uint32_t)r ? (((uint32_t)key[k] & 0x7FFu) | (len[k] << 11)) : kl;
+    for (int k = 0; k < CAP; k++)
+      kl = crank[k] == (uint32_t)r ? (((uint32_t)key[k] & 0x7FFu) | (len[k] << 11)) : kl;
+    TK[r >> 1] |= kl << (16 * (r & 1));
+  }
+  S.hdr = nbits | (table_bytes << 16);
+  S.size = 3 + table_bytes + (nbits + 7) / 8;
+  S.n = n;
+  S.msz = (uint32_t)msz;
+  S.lcount = lcount;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    S.TK[j] = TK[j];
+    S.CT[j] = j < NP ? CT[j < NP ? j : 0] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < SlotIds<8>::kRegs; j++) S.ids.r[j] = ids.r[j];
+  R8_STAMP(4);
+  return true;
+}
+
+// The chunk bytes of a built block (Huffman::dump, Huffman.cpp:279-326):
+// header, 11-bit table groups (one per code length: <= 8 symbols), code bits
+// of the message in position order.  W: DenseWriter (K2's tile run) or a
+// host-side writer with the same put / align_byte.
+template <class W>
+MYYUV_HD void emit_chunk(const EncState& S, int wave_msz, W& bw) {
+  bw.put(S.hdr, 24);
+  uint32_t curlen = 0;
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    if ((uint32_t)r < S.n) {
+      const uint32_t kl = (S.TK[r >> 1] >> (16 * (r & 1))) & 0xFFFFu;
       const uint32_t L = kl >> 11;
       if (L != curlen) {
         bw.align_byte();
-        const uint32_t c = (uint32_t)(lcount >> (8 * (L - 1))) & 0xFFu;
+        const uint32_t c = (uint32_t)(S.lcount >> (8 * (L - 1))) & 0xFFu;
         bw.put(((L - 1) << 5) | (c - 1), 8);
         curlen = L;
       }
@@ -482,17 +562,13 @@ MYYUV_HD bool encode_block_r(const CoefRegs& R, int msz, int wave_msz,
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int i = i0 + k;
-        if (i < msz) {
-          const uint32_t ct = f16<CAP>(CT, ids.get(i));
+        if ((uint32_t)i < S.msz) {
+          const uint32_t ct = rr::f16<8>(S.CT, S.ids.get(i));
           bw.put(ct & 0xFFu, (int)(ct >> 8));
         }
       }
     }
   }
-  bw.flush();
-  *size_out = (uint8_t)(3 + table_bytes + (nbits + 7) / 8);
-  R8_STAMP(5);
-  return true;
 }
 
 // K2 block classes (k_huff_encode sorts a workgroup's blocks by class so each
@@ -514,12 +590,17 @@ MYYUV_HD uint32_t block_class(const CoefRegs& R, int msz) {
 // coefficient alone; Huffman.cpp:191-194 for the all-zero case): one code of
 // length 1, one table group; the chunk is 7 bytes:
 //   u16 nbits = 1, u8 table_bytes = 3, group header 0x00, 11-bit key, 1 code byte 0.
-MYYUV_HD void encode_block_single(const CoefRegs& R, uint32_t* __restrict__ slot,
-                                  uint8_t* __restrict__ size_out) {
-  const uint32_t key = (uint32_t)R.sym(0) & 0x7FFu;
-  slot[0] = 1u | (3u << 16);
-  slot[kWave] = key;
-  *size_out = 7;
+MYYUV_HD void build_single(const CoefRegs& R, EncState& S) {
+  S.hdr = 1u | (3u << 16);
+  S.size = 7;
+  S.n = 1;
+  S.msz = 1;
+  S.lcount = 1;
+  S.TK[0] = ((uint32_t)R.sym(0) & 0x7FFu) | (1u << 11);
+  S.TK[1] = S.TK[2] = S.TK[3] = 0u;
+  S.CT[0] = 1u << 8;  // length 1, code 0
+  S.CT[1] = S.CT[2] = S.CT[3] = 0u;
+  S.ids.clear();
 }
 
 }  // namespace myyuv_gpu

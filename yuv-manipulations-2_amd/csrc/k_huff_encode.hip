@@ -565,7 +565,8 @@ __device__ __forceinline__ void put_bits(uint32_t* img, uint32_t off, uint32_t v
 
 __device__ void encode_block_wave(const uint4* __restrict__ coef, const uint8_t* __restrict__ rmask, uint32_t g,
                                   uint32_t* img,
-                                  uint32_t* __restrict__ slots, uint8_t* __restrict__ sizes,
+                                  uint32_t* __restrict__ oslots, uint8_t* __restrict__ sizes,
+                                  uint32_t* __restrict__ tile_bytes,
                                   uint32_t _wslot = 0) {
   const uint32_t lane = threadIdx.x;
 #ifdef MYYUV_STAMPS
@@ -708,9 +709,12 @@ __device__ void encode_block_wave(const uint4* __restrict__ coef, const uint8_t*
   }
   if (act) put_bits(img, 8 * (3 + table_bytes) + pre - pl, pc, pl);
   __builtin_amdgcn_wave_barrier();
-  if (lane < (uint32_t)kSlotWords)
-    slots[(size_t)(g >> 6) * (kSlotWords * kWave) + lane * kWave + (g & 63)] = img[lane];
-  if (lane == 0) sizes[g] = (uint8_t)(3 + table_bytes + (nbits + 7) / 8);
+  if (lane < (uint32_t)kSlotWords) oslots[(size_t)g * kSlotWords + lane] = img[lane];
+  if (lane == 0) {
+    const uint32_t size = 3 + table_bytes + (nbits + 7) / 8;
+    sizes[g] = (uint8_t)size;
+    atomicAdd(tile_bytes, size);  // the tile's overflow chunk bytes (K4's tile scan)
+  }
   WSTAMP(7);
 }
 
@@ -720,53 +724,71 @@ __device__ void encode_block_wave(const uint4* __restrict__ coef, const uint8_t*
 // encode_block_wave); exits at once when the list is long (the lane pass
 // k_huff_encode_wide takes it).
 __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict__ coef,
-                                                        const uint8_t* __restrict__ rmask,
-                                                        uint32_t* __restrict__ slots,
+                                                        const uint8_t* __restrict__ rmask, FrameGeom G,
+                                                        uint32_t* __restrict__ oslots,
                                                         uint8_t* __restrict__ sizes,
+                                                        uint32_t* __restrict__ tinfo,
                                                         const uint32_t* __restrict__ work,
                                                         const uint32_t* __restrict__ work_count,
                                                         uint32_t limit) {
   __shared__ uint32_t img[kSlotWords + 2];
   const uint32_t cnt = *work_count;
   if (cnt > limit) return;
-  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) encode_block_wave(coef, rmask, work[i], img, slots, sizes, i);
+  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const uint32_t g = work[i];
+    encode_block_wave(coef, rmask, g, img, oslots, sizes, tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, i);
+  }
 }
 
-// Fast pass over every block.  A workgroup takes kK2Group consecutive blocks,
-// classifies them (block_class: one symbol / <= 4 / <= 8 distinct for sure /
-// the rest), sorts them by class through LDS and hands each wave 64 blocks of
-// (nearly) one class, so a wave runs the cheapest register-resident encoder
-// that fits all its blocks and its loops run to the maxima of similar blocks
-// rather than of a 64-block stretch of the frame.  Sorted chunks are dealt to
-// the waves so that each SIMD gets one heavy and one light chunk.  Blocks with
-// more than 8 distinct symbols are appended to `work` for the overflow passes.
-//   coef: natural-order quads (codec_common.hpp);
-//   slots: [ceil(n/64)][40][64] u32; sizes: [n] u8.
+// Fast pass over every block, one workgroup per tile (kK2Group consecutive
+// blocks of one plane of one frame: FrameGeom::tcum; grid (tiles, frames)).
+// The workgroup classifies its blocks (block_class: one symbol / <= 4 / <= 8
+// distinct for sure / the rest), sorts them by class through LDS and hands
+// each wave 64 blocks of (nearly) one class, so a wave runs the cheapest
+// register-resident encoder that fits all its blocks and its loops run to the
+// maxima of similar blocks rather than of a 64-block stretch of the frame.
+// Sorted chunks are dealt to the waves so that each SIMD gets one heavy and
+// one light chunk.  Each lane builds its block's code (sizes known before a
+// bit is written), a wave scan gives every chunk its byte offset, and the
+// wave's chunks go back to back into its dense run (DenseWriter: every dword
+// stored once, by the block owning its first byte); srcoff records where
+// each block's chunk is (codec_common.hpp, K2 -> K4).  Blocks with more than
+// 8 distinct symbols are appended to `work` for the overflow passes.
+//   coef: natural-order quads (codec_common.hpp); sizes: [n] u8.
 #ifndef MYYUV_K2_WAVES
 #define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (a few spills; +2.6 % in the bench, tools/ab_bench.sh)
 #endif
 __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
                                                          const uint8_t* __restrict__ rmask,
-                                                         const uint4* __restrict__ zq,
-                                                         uint32_t nblocks,
-                                                         uint32_t* __restrict__ slots,
+                                                         const uint4* __restrict__ zq, FrameGeom G,
+                                                         uint32_t* __restrict__ stage,
+                                                         uint32_t* __restrict__ tinfo,
                                                          uint8_t* __restrict__ sizes,
+                                                         uint16_t* __restrict__ srcoff,
                                                          uint32_t* __restrict__ work,
                                                          uint32_t* __restrict__ work_count) {
   constexpr int kWaves = kK2Group / kWave;
-  __shared__ uint32_t s_g[kK2Group];
+  __shared__ uint32_t s_g[kK2Group];  // sorted position -> the tile's block
   __shared__ uint8_t s_msz[kK2Group], s_cls[kK2Group], s_rm[kK2Group];
   __shared__ uint32_t s_cnt[kWaves][kClassDead + 1];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t t = blockIdx.x, f = blockIdx.y;
+  const uint32_t T = f * G.tcum[3] + t;  // batch tile
+  const int p = tile_plane(G, t);
+  const uint32_t g0 = tile_first(G, p, t);
+  const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
+  const uint32_t gb = f * G.cum[3] + g0;  // batch-global index of the tile's block 0
+  // the overflow passes add their chunk bytes to the tile's info word 0
+  // (ordered before them by the kernel boundary)
+  if (tid == 0) tinfo[(size_t)T * kTInfoWords] = 0u;
   // ---- classify
-  const uint32_t g = blockIdx.x * kK2Group + tid;
   uint32_t cls = kClassDead;
   int msz = 0;
   uint32_t rm = 0;
-  if (g < nblocks) {
-    rm = rmask[g];
+  if (tid < nloc) {
+    rm = rmask[gb + tid];
     CoefRegs R;
-    R.load(coef, zq, g, rm);
+    R.load(coef, zq, gb + tid, rm);
     msz = R.msz();
     cls = block_class(R, msz);
   }
@@ -786,51 +808,83 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
 #pragma unroll
     for (uint32_t w = 0; w < (uint32_t)kWaves; w++)
       pos += (c < cls || (c == cls && w < wave)) ? s_cnt[w][c] : 0u;
-  s_g[pos] = g;
+  s_g[pos] = tid;
   s_msz[pos] = (uint8_t)msz;
   s_cls[pos] = (uint8_t)cls;
   s_rm[pos] = (uint8_t)rm;
   __syncthreads();
-  // ---- encode: wave w takes sorted chunk w < kWaves/2 ? kWaves-1-w : w-kWaves/2
+  // ---- build: wave w takes sorted chunk w < kWaves/2 ? kWaves-1-w : w-kWaves/2
   const uint32_t chunk = wave < (uint32_t)kWaves / 2 ? kWaves - 1 - wave : wave - kWaves / 2;
   const uint32_t e = chunk * kWave + lane;
-  const uint32_t mg = s_g[e];
+  const uint32_t ml = s_g[e];  // the lane's block in the tile (every one of 0..255 once)
   const int mm = s_msz[e];
   const uint32_t mc = s_cls[e];
   const bool live = mc != kClassDead;
+  const uint32_t mg = gb + ml;
   uint32_t wcls = kClassDead;  // the wave's heaviest live class
 #pragma unroll
   for (int c = kClassDead - 1; c >= 0; c--)
     if (wcls == kClassDead && __ballot(mc == (uint32_t)c) != 0) wcls = (uint32_t)c;
-  if (wcls == kClassDead) return;
   const int wmsz = max(wave_max(live ? mm : 0), 1);
 #ifdef MYYUV_STAMPS
-  if (lane == 0 && blockIdx.x * kWaves + wave < 8192) g_k2_fstamps[(blockIdx.x * kWaves + wave) * 8 + 0] = wcls | ((uint32_t)wmsz << 8);
+  const uint32_t wid = (f * G.tcum[3] + t) * kWaves + wave;
+  if (lane == 0 && wid < 8192) g_k2_fstamps[wid * 8 + 0] = wcls | ((uint32_t)wmsz << 8);
   const unsigned long long _w0 = __builtin_amdgcn_s_memtime();
 #endif
-  CoefRegs R;
-  R.load(coef, zq, live ? mg : 0u, live ? s_rm[e] : 0u);
-  uint32_t* slot = slots + (size_t)(mg >> 6) * (kSlotWords * kWave) + (mg & 63);
-  uint8_t* so = sizes + mg;
-  bool ok = true;
-  if (wcls == kClassSingle) {
-    if (live) encode_block_single(R, slot, so);
-  } else if (wcls == kClassR4) {
-    if (live) ok = encode_block_r<4>(R, mm, wmsz, slot, so);
-  } else {
-    if (live) ok = encode_block_r<8>(R, mm, wmsz, slot, so);
+  EncState S;
+  bool ok = false;
+  if (wcls != kClassDead) {
+    CoefRegs R;
+    R.load(coef, zq, live ? mg : gb, live ? s_rm[e] : 0u);
+    if (wcls == kClassSingle) {
+      if (live) {
+        build_single(R, S);
+        ok = true;
+      }
+    } else if (wcls == kClassR4) {
+      if (live) ok = build_r<4>(R, mm, wmsz, S);
+    } else {
+      if (live) ok = build_r<8>(R, mm, wmsz, S);
+    }
   }
-#ifdef MYYUV_STAMPS
-  if (lane == 0 && blockIdx.x * kWaves + wave < 8192)
-    g_k2_fstamps[(blockIdx.x * kWaves + wave) * 8 + 7] = (uint32_t)(__builtin_amdgcn_s_memtime() - _w0);
-#endif
+  // ---- the wave's dense run: chunks back to back in the wave's order
+  // (offsets by a wave scan of the sizes; no workgroup barrier), every dword
+  // stored once (DenseWriter)
+  const bool dense = live && ok;
+  const uint32_t sz = dense ? S.size : 0u;
+  uint32_t incl = sz;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+    if (lane >= (uint32_t)d) incl += o;
+  }
+  const uint32_t off = incl - sz;
+  const uint64_t dm = __ballot(dense);
+  const uint64_t above = lane == 63 ? 0ull : dm & ~((2ull << lane) - 1ull);
+  const int nl = above ? __ffsll((long long)above) - 1 : (int)lane;
+  const uint32_t nhdr = (uint32_t)__shfl((int)(dense ? S.hdr : 0u), nl, 64);
+  uint32_t* info = tinfo + (size_t)T * kTInfoWords;
+  if (lane == 63) info[1 + wave] = incl;  // the run's bytes
+  if (dense) {
+    DenseWriter dw;
+    dw.init(stage + (size_t)T * (kTileCap / 4) + wave * (kWaveRun / 4), off);
+    emit_chunk(S, wmsz, dw);
+    dw.finish(above ? (nhdr | 0x80000000u) : 0u);
+    sizes[mg] = (uint8_t)S.size;
+    srcoff[mg] = (uint16_t)(wave * kWaveRun + off);
+  }
+  // blocks with more than 8 distinct symbols: the overflow passes' worklist
   const uint64_t ovf = __ballot(live && !ok);
   if (ovf) {
+    if (live && !ok) srcoff[mg] = kSrcOverflow;
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(work_count, (uint32_t)__popcll(ovf));
     base = __builtin_amdgcn_readfirstlane(base);
     if ((ovf >> lane) & 1) work[base + (uint32_t)__popcll(ovf & below)] = mg;
   }
+#ifdef MYYUV_STAMPS
+  if (lane == 0 && wid < 8192) g_k2_fstamps[wid * 8 + 7] = (uint32_t)(__builtin_amdgcn_s_memtime() - _w0);
+#endif
 }
 
 // Overflow pass (CAP=64), lane per block, for long worklists (noise-like
@@ -839,9 +893,10 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
 // groups exit.  Lists of at most `limit` blocks go to k_huff_encode_wave instead.
 __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict__ coef,
                                                         const uint8_t* __restrict__ rmask,
-                                                        const uint4* __restrict__ zq,
-                                                        uint32_t* __restrict__ slots,
+                                                        const uint4* __restrict__ zq, FrameGeom G,
+                                                        uint32_t* __restrict__ oslots,
                                                         uint8_t* __restrict__ sizes,
+                                                        uint32_t* __restrict__ tinfo,
                                                         const uint32_t* __restrict__ work,
                                                         const uint32_t* __restrict__ work_count,
                                                         uint32_t limit) {
@@ -861,8 +916,8 @@ __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict
     const int wmsz = wave_max(msz);
     if (live) {
       const Img<CAP> I{lds, (int)threadIdx.x};
-      encode_block<CAP>(I, R, msz, max(wmsz, 1),
-                        slots + (size_t)(g >> 6) * (kSlotWords * kWave) + (g & 63), sizes + g);
+      encode_block<CAP>(I, R, msz, max(wmsz, 1), oslots + (size_t)g * kSlotWords, sizes + g);
+      atomicAdd(tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, (uint32_t)sizes[g]);  // (this lane's own store)
     }
   }
 }

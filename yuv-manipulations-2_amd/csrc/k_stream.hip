@@ -2,9 +2,10 @@
 //   * k_scan_chain: exclusive scan of the u8 chunk sizes in one pass
 //     (DCTYUVPlane::getContentPos, DCT.cpp:21-33, done for all planes at once),
 //     decode side with the stream header checks;
-//   * k_compact: chunk slots -> the DCTYUV byte stream (DCTYUV::dump /
-//     DCTYUVPlane::dumpTo, DCT.cpp:63-73, 160-173, and the serial compaction of
-//     applyDCTPlane, :314-322);
+//   * k_tile_scan + k_stream_out: K2's tiles -> the DCTYUV byte stream
+//     (DCTYUV::dump / DCTYUVPlane::dumpTo, DCT.cpp:63-73, 160-173, and the
+//     serial compaction of applyDCTPlane, :314-322): a scan of per-tile
+//     totals, then the chunks of each tile;
 //
 // Stream layout: u32 plane_size[3]; per plane p:
 //   u32 nblocks, u32 content_size, u8 chunk_size[nblocks], u8 content[...].
@@ -135,96 +136,174 @@ __device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uin
   return local_off[g] + tile_pre[g / kScanTile];
 }
 
-// Compaction: one workgroup = up to 256 consecutive blocks of one plane of
-// frame blockIdx.y, one lane per block (chunk).
-__global__ __launch_bounds__(256) void k_compact(const uint32_t* __restrict__ slots,
-                                                const uint8_t* __restrict__ sizes,
-                                                const uint32_t* __restrict__ local_off,
-                                                const uint32_t* __restrict__ tile_pre,
-                                                FrameGeom G, uint32_t tiles_p0, uint32_t tiles_p1,
-                                                uint8_t* __restrict__ out, uint32_t cap,
-                                                uint32_t* __restrict__ out_size,
-                                                unsigned long long* __restrict__ err) {
-  // frame blockIdx.y of the batch: slots / sizes at batch-global block
-  // gbase + g, its scan, its output slot of `cap` bytes
-  const uint32_t f = blockIdx.y, gbase = f * G.cum[3];
-  const uint32_t ntiles = (G.cum[3] + kScanTile - 1) / kScanTile;
-  sizes += gbase;
-  local_off += gbase;
-  tile_pre += (size_t)f * (ntiles + 1);
-  out += (size_t)f * cap;
-  out_size += f;
-  const uint32_t t = blockIdx.x;
-  const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
-  const uint32_t tile_in_plane = t - (p == 0 ? 0 : (p == 1 ? tiles_p0 : tiles_p0 + tiles_p1));
-  const uint32_t g0 = G.cum[p] + tile_in_plane * 256;
-  const uint32_t g1 = min(g0 + 256, G.cum[p + 1]);
-  const uint32_t plane_pre = scanned(local_off, tile_pre, G.cum[p]);
-  const uint32_t total_content = tile_pre[(G.cum[3] + kScanTile - 1) / kScanTile];
-  const uint64_t total = 12ull + 24ull + G.cum[3] + total_content;
-
-  // headers: first workgroup of each plane
-  if (g0 == G.cum[p] && threadIdx.x < 3) {
-    const uint32_t next_pre = p < 2 ? scanned(local_off, tile_pre, G.cum[p + 1]) : total_content;
-    const uint32_t nb = G.cum[p + 1] - G.cum[p];
-    const uint32_t content = next_pre - plane_pre;
-    if (threadIdx.x == 0 && total <= cap) {
-      const uint64_t hpos = 12ull + 8ull * p + G.cum[p] + plane_pre;
+// Compress side, after K2 and the overflow passes (codec_common.hpp, K2 -> K4):
+//   k_tile_scan: one workgroup per frame: the exclusive scan of the frame's
+//     tile totals (the tiles' share of DCTYUVPlane::getContentPos, DCT.cpp:21-33),
+//     the plane headers and plane sizes (DCTYUVPlane::dumpTo / DCTYUV::dump,
+//     DCT.cpp:63-73, 160-173) and the payload size;
+//   k_stream_out: one workgroup per tile: the chunk_size[] bytes and the
+//     chunks in block order (applyDCTPlane's serial compaction, :314-322).
+// A frame has ~1.1k tiles (4032x3008): one workgroup scans them in a few
+// passes, so no look-back chain is needed anywhere.
+__global__ __launch_bounds__(1024) void k_tile_scan(uint32_t* __restrict__ tinfo, FrameGeom G,
+                                                   uint8_t* __restrict__ out, uint32_t cap,
+                                                   uint32_t* __restrict__ out_size,
+                                                   unsigned long long* __restrict__ err) {
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_carry;
+  const uint32_t f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t ntile = G.tcum[3];
+  uint32_t* info = tinfo + (size_t)f * ntile * kTInfoWords;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < ntile; base += 1024) {
+    const uint32_t t = base + tid;
+    uint32_t v = 0;
+    if (t < ntile) {
+      const uint32_t* w = info + (size_t)t * kTInfoWords;
+      v = w[0] + w[1] + w[2] + w[3] + w[4];
+    }
+    const uint32_t incl = wave_inclusive_scan(v);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t pre = s_carry, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+      pre += k < wave ? s_w[k] : 0u;
+      tot += s_w[k];
+    }
+    if (t < ntile) info[(size_t)t * kTInfoWords + kTInfoPrefix] = pre + incl - v;
+    __syncthreads();
+    if (tid == 0) s_carry += tot;
+    __syncthreads();
+  }
+  // plane headers: the prefixes at the planes' first tiles (written above by
+  // this workgroup; __syncthreads orders them)
+  if (tid < 3) {
+    const int p = (int)tid;
+    const uint32_t total = s_carry;
+    const uint32_t ppre = info[(size_t)G.tcum[p] * kTInfoWords + kTInfoPrefix];
+    const uint32_t pend = p < 2 ? info[(size_t)G.tcum[p + 1] * kTInfoWords + kTInfoPrefix] : total;
+    const uint32_t nb = G.cum[p + 1] - G.cum[p], content = pend - ppre;
+    uint8_t* o = out + (size_t)f * cap;
+    const uint64_t hpos = 12ull + 8ull * p + G.cum[p] + ppre;
+    if (hpos + 8 <= cap) {
       const uint32_t vals[2] = {nb, content};
-      for (int k = 0; k < 8; k++) out[hpos + k] = (uint8_t)(vals[k >> 2] >> (8 * (k & 3)));
-      const uint32_t psize = 8 + nb + content;
-      for (int k = 0; k < 4; k++) out[4 * p + k] = (uint8_t)(psize >> (8 * k));
+      for (int k = 0; k < 8; k++) o[hpos + k] = (uint8_t)(vals[k >> 2] >> (8 * (k & 3)));
     }
-    if (p == 0 && threadIdx.x == 1) {
-      *out_size = (uint32_t)total;
-      if (total > cap) record_error(err, 0, 5 /* MYYUV_E_CAPACITY */);  // any frame
+    const uint32_t psize = 8 + nb + content;
+    for (int k = 0; k < 4; k++) o[4 * p + k] = (uint8_t)(psize >> (8 * k));
+    if (p == 0) {
+      const uint64_t bytes = 12ull + 24ull + G.cum[3] + total;
+      out_size[f] = (uint32_t)bytes;
+      if (bytes > cap) record_error(err, 0, 5 /* MYYUV_E_CAPACITY, any frame */);
     }
   }
-  if (total > cap) return;
+}
 
-  const uint32_t g = g0 + threadIdx.x;
-  if (g >= g1) return;
-  const uint32_t sz = sizes[g];
-  out[12ull + 8ull * (p + 1) + plane_pre + g] = (uint8_t)sz;  // chunk_size[k]
-  // The chunk's bytes [pos, end) go straight to the stream: the image words
-  // strictly inside the range are this lane's alone (dword stores); the first
-  // and last words can hold a neighbour's bytes, so only this chunk's bytes of
-  // them are stored (byte stores: no read-modify-write, no atomics, no LDS).
-  // Slot words are loaded 8 at a time with no predication (a slot is always
-  // kSlotWords = 5 x 8 words long): one HBM round trip per batch.
-  const uint64_t pos = 12ull + 8ull * (p + 1) + G.cum[p + 1] + scanned(local_off, tile_pre, g);
-  const uint64_t end = pos + sz;
-  const uint64_t a0 = pos & ~3ull, al = (end - 1) & ~3ull;
-  const uint32_t sh = (uint32_t)(pos & 3) * 8;
-  const uint32_t ga = gbase + g;
-  const uint32_t* slot = slots + (size_t)(ga / kWave) * (kSlotWords * kWave) + (ga % kWave);
-  const uint32_t nw = (sz + 3) >> 2;
-  if (nw == 0) return;  // (a chunk is at least 7 bytes; a corrupt size of 0 writes nothing)
-  auto edge = [&](uint64_t a, uint32_t v) {
+// One tile: its chunks, in block order, from the K2 runs / overflow slots
+// straight into the stream, one lane per block.  Every stream dword inside a
+// plane's content is stored once, by the chunk owning its first byte, with
+// the next chunk's first bytes — at most 3, so always the next chunk's header
+// (u16 nbits, u8 table_bytes), which the next lane loads anyway — completing
+// its last dword.  Only where the content meets other data (a plane's size
+// array before its first chunk, the next plane's header after its last) are
+// the shared dwords written with byte stores.  No LDS image, no atomics.
+__global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__ stage,
+                                                    const uint32_t* __restrict__ tinfo,
+                                                    const uint8_t* __restrict__ sizes,
+                                                    const uint16_t* __restrict__ srcoff,
+                                                    const uint32_t* __restrict__ oslots, FrameGeom G,
+                                                    uint8_t* __restrict__ out, uint32_t cap) {
+  __shared__ uint32_t s_wt[4], s_hdr[4];
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t t = blockIdx.x, f = blockIdx.y, ntile = G.tcum[3];
+  const uint32_t T = f * ntile + t;
+  const int p = tile_plane(G, t);
+  const uint32_t g0 = tile_first(G, p, t);
+  const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
+  const uint32_t gb = f * G.cum[3] + g0;
+  out += (size_t)f * cap;
+  const uint32_t x = tinfo[(size_t)T * kTInfoWords + kTInfoPrefix];  // the tile's content prefix
+  const uint32_t ppre = tinfo[((size_t)f * ntile + G.tcum[p]) * kTInfoWords + kTInfoPrefix];
+  // the lane's block, and for the tile's last block the next tile's first
+  // (its header completes the last dword when the plane goes on)
+  const bool live = tid < nloc;
+  const bool plane_end = g0 + nloc == G.cum[p + 1];
+  const uint32_t sz = live ? sizes[gb + tid] : 0u;
+  const uint32_t so = live ? srcoff[gb + tid] : 0u;
+  const uint32_t* src;
+  uint32_t sh;  // source byte misalignment
+  if (so == kSrcOverflow) {
+    src = oslots + (size_t)(gb + tid) * kSlotWords;
+    sh = 0;
+  } else {
+    src = stage + (size_t)T * (kTileCap / 4) + (so >> 2);
+    sh = so & 3u;
+  }
+  uint32_t nxh = 0;  // the next tile's first header (lane nloc - 1, plane going on)
+  if (tid == nloc - 1 && !plane_end) {
+    const uint32_t so1 = srcoff[gb + nloc];
+    const uint32_t* s1 = so1 == kSrcOverflow ? oslots + (size_t)(gb + nloc) * kSlotWords
+                                             : stage + (size_t)(T + 1) * (kTileCap / 4) + (so1 >> 2);
+    const uint32_t r1 = so1 == kSrcOverflow ? 0u : so1 & 3u;
+    nxh = r1 ? (s1[0] >> (8 * r1)) | (s1[1] << (32 - 8 * r1)) : s1[0];
+  }
+  // source words 8 (+1) per load round trip; the first round also gives the
+  // chunk's header
+  const uint32_t nsrc = (sh + sz + 3) >> 2;
+  uint32_t v[9];
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (a + k >= pos && a + k < end) out[a + k] = (uint8_t)(v >> (8 * k));
+  for (uint32_t k = 0; k < 9; k++) v[k] = (k < nsrc) ? src[k] : 0u;
+  const uint32_t hdr = sh ? (v[0] >> (8 * sh)) | (v[1] << (32 - 8 * sh)) : v[0];
+  // ---- offsets in the tile (block order), the next lane's header
+  const uint32_t incl = wave_inclusive_scan(sz);
+  if (lane == 63) s_wt[wave] = incl;
+  if (lane == 0) s_hdr[wave] = hdr;
+  __syncthreads();
+  uint32_t o = incl - sz;
+#pragma unroll
+  for (uint32_t w = 0; w < 4; w++) o += w < wave ? s_wt[w] : 0u;
+  uint32_t nh = (uint32_t)__shfl_down((int)hdr, 1, 64);
+  if (lane == 63) nh = wave < 3 ? s_hdr[wave + 1] : 0u;
+  if (tid == nloc - 1) nh = nxh;
+  const bool has_next = tid + 1 < nloc || !plane_end;  // a chunk follows in this plane
+  // ---- chunk_size[] bytes (DCTYUVPlane layout: after the plane's 8-byte header)
+  const uint64_t spos = 12ull + 8ull * (p + 1) + ppre + g0;
+  if (live && spos + tid < cap) out[spos + tid] = (uint8_t)sz;
+  if (!live || sz == 0) return;
+  const uint64_t P = 12ull + 8ull * (p + 1) + G.cum[p + 1] + x + o;  // the chunk's stream position
+  if (P + sz > cap) return;  // (capacity: k_tile_scan reports it)
+  // ---- chunk bytes k .. k+3 (from source byte sh + k), the next header after byte sz
+  auto word_at = [&](uint32_t k, const uint32_t* w, uint32_t j0) -> uint32_t {
+    const uint32_t r = sh + k, i = (r >> 2) - j0, q = r & 3u;
+    return q ? (w[i] >> (8 * q)) | (w[i + 1] << (32 - 8 * q)) : w[i];
   };
-  uint32_t carry = 0;  // bits of the previous slot word shifted past its stream word
-  for (uint32_t j0 = 0; j0 < nw; j0 += 8) {
-    uint32_t d[8];
+  const uint32_t lead = (uint32_t)((4u - (uint32_t)(P & 3u)) & 3u);  // chunk bytes before the first own dword
+  const bool plane_first = g0 + tid == G.cum[p];
+  if (plane_first && lead) {  // the dword before is shared with the size array
+    const uint32_t w = word_at(0, v, 0);
+    for (uint32_t k = 0; k < lead; k++) out[P + k] = (uint8_t)(w >> (8 * k));
+  }
+  uint32_t j0 = 0;  // first source word held in v
+  for (uint32_t k = lead; k < sz; k += 4) {
+    const uint32_t need = (sh + k) >> 2;
+    if (need + 1 >= j0 + 9) {  // refill (chunks over ~28 bytes)
+      j0 = need;
 #pragma unroll
-    for (int k = 0; k < 8; k++) d[k] = slot[(j0 + k) * kWave];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t j = j0 + k;
-      if (j < nw) {
-        const uint32_t v = sh ? (d[k] << sh) | carry : d[k];
-        carry = sh ? d[k] >> (32 - sh) : 0u;
-        const uint64_t a = a0 + 4ull * j;
-        if (a == a0 || a == al)
-          edge(a, v);
-        else
-          *reinterpret_cast<uint32_t*>(out + a) = v;
-      }
+      for (uint32_t i = 0; i < 9; i++) v[i] = (j0 + i < nsrc) ? src[j0 + i] : 0u;
+    }
+    uint32_t w = word_at(k, v, j0);
+    const uint32_t rem = sz - k;
+    if (rem >= 4) {
+      *reinterpret_cast<uint32_t*>(out + P + k) = w;
+    } else if (has_next && P + k + 4 <= cap) {  // complete the dword with the next chunk's first bytes
+      w = (w & ((1u << (8 * rem)) - 1u)) | (nh << (8 * rem));
+      *reinterpret_cast<uint32_t*>(out + P + k) = w;
+    } else {  // the plane's last chunk (the next plane's header follows), or the end of `cap`
+      for (uint32_t i = 0; i < rem; i++) out[P + k + i] = (uint8_t)(w >> (8 * i));
     }
   }
-  if (a0 + 4ull * nw == al) edge(al, carry);
 }
 
 }  // namespace myyuv_gpu

@@ -2,7 +2,7 @@
 //
 // Host side of the gfx950 codec: frame geometry, quantisation tables, the
 // per-context workspace, and the launch sequences
-//   compress:   K1 fdct_quant -> K2 huff_encode -> scan -> K4 compact
+//   compress:   K1 fdct_quant -> K2 huff_encode (+ overflow pass) -> K4 stream_out
 //   decompress: parse -> scan -> K5 huff_decode -> K6 dequant_idct
 // Every launch goes to one stream; nothing synchronises inside the
 // device-resident entry points, so frames pipeline back to back.
@@ -25,18 +25,18 @@ namespace myyuv_gpu {
 __global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*);
 __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*,
                                uint4*);
-__global__ void k_huff_encode(const uint4*, const uint8_t*, const uint4*, uint32_t, uint32_t*, uint8_t*,
-                              uint32_t*, uint32_t*);
-__global__ void k_huff_encode_wave(const uint4*, const uint8_t*, uint32_t*, uint8_t*, const uint32_t*,
-                                   const uint32_t*, uint32_t);
-__global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, uint32_t*, uint8_t*,
+__global__ void k_huff_encode(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
+                              uint8_t*, uint16_t*, uint32_t*, uint32_t*);
+__global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
                                    const uint32_t*, const uint32_t*, uint32_t);
+__global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
+                                   uint32_t*, const uint32_t*, const uint32_t*, uint32_t);
+__global__ void k_tile_scan(uint32_t*, FrameGeom, uint8_t*, uint32_t, uint32_t*, unsigned long long*);
 __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
                              StreamDesc*, uint32_t*, uint32_t*, uint32_t, unsigned long long*,
                              uint32_t, unsigned long long*);
-__global__ void k_compact(const uint32_t*, const uint8_t*, const uint32_t*, const uint32_t*,
-                          FrameGeom, uint32_t, uint32_t, uint8_t*, uint32_t, uint32_t*,
-                          unsigned long long*);
+__global__ void k_stream_out(const uint32_t*, const uint32_t*, const uint8_t*, const uint16_t*,
+                             const uint32_t*, FrameGeom, uint8_t*, uint32_t);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
                               uint4*, uint8_t*, unsigned long long*);
@@ -134,6 +134,7 @@ int make_geom(uint32_t w, uint32_t h, FrameGeom& G) {
     G.cum[p + 1] = G.cum[p] + G.bw[p] * (ph[p] / 8);
     G.bmag[p] = block_magic(G.bw[p]);
     G.ucum[p + 1] = G.ucum[p] + ceil_div(G.cum[p + 1] - G.cum[p], kXfUnit);
+    G.tcum[p + 1] = G.tcum[p] + ceil_div(G.cum[p + 1] - G.cum[p], kK2Group);
   }
   G.poff[0] = 0;
   G.poff[1] = w * h;
@@ -165,7 +166,8 @@ struct myyuv_hip_ctx {
   // on different streams through one context run in call order.
   hipEvent_t done = nullptr;
   hipStream_t last_stream = nullptr;
-  DevBuf frame, coef, slots, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
+  DevBuf frame, coef, sizes, loff, tiles, payload, err, psize, desc, work, qtd;
+  DevBuf stage, oslots, tinfo, srcoff;  // K2 -> K4 (codec_common.hpp)
   DevBuf bmp;   // staged BMP pixels (host-buffer BMP -> IYUV)
   DevBuf bsizes;  // u32 payload sizes of a host-buffer batch
   DevBuf rmask; // per block: bit c = coefficient row c nonzero (K5 -> K6)
@@ -297,7 +299,10 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   const uint32_t ntiles = ceil_div(G.cum[3], kScanTile);
   int e = 0;
   e |= c->coef.grow((size_t)nwaves * kCoefQuadsPerWave * 16);  // natural-order quads
-  e |= c->slots.grow((size_t)nwaves * kSlotWords * kWave * 4);
+  e |= c->stage.grow((size_t)nf * G.tcum[3] * kTileCap);
+  e |= c->oslots.grow((size_t)nblk * kMaxChunk);
+  e |= c->tinfo.grow((size_t)nf * G.tcum[3] * kTInfoWords * 4);
+  e |= c->srcoff.grow((size_t)nblk * 2);
   e |= c->sizes.grow((size_t)nwaves * kWave);
   e |= c->rmask.grow((size_t)nblk);
   if (c->zq.n == 0) {
@@ -327,29 +332,33 @@ uint32_t next_epoch(myyuv_hip_ctx* c) {
   return c->epoch;
 }
 
-// K2: fast pass over all blocks, then the overflow pass over the blocks with
-// more than 8 distinct symbols (worklist filled on the device; no host sync):
-// wave-per-block for lists of at most kWaveEncodeLimit blocks, lane-per-block
-// for longer ones; both kernels are queued and each returns at once outside
-// its regime.  A batch (nf > 1) takes the lane-per-block pass only: its list
-// is long, and the wave pass's per-block SALU cost would crowd the other
-// launch groups in flight (tools/kskip.py).
-int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, uint32_t nf, hipStream_t s) {
+// K2: fast pass over all tiles (grid (tiles, frames)), then the overflow pass
+// over the blocks with more than 8 distinct symbols (worklist filled on the
+// device; no host sync): wave-per-block for lists of at most kWaveEncodeLimit
+// blocks, lane-per-block for longer ones; both kernels are queued and each
+// returns at once outside its regime.  A batch (nf > 1) takes the
+// lane-per-block pass only: its list is long, and the wave pass's per-block
+// SALU cost would crowd the other launch groups in flight (tools/kskip.py).
+int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
+  const uint32_t nf = G.nframes, nblk = G.cum[3] * nf;
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
   const uint32_t limit = nf > 1 ? 0u : kWaveEncodeLimit;
-  int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(ceil_div(nblk, kK2Group)), dim3(kK2Group), s,
-                 c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), nblk, c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
-                 list, count);
+  int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(G.tcum[3], nf), dim3(kK2Group), s,
+                 c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
+                 c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
+                 c->srcoff.as<uint16_t>(), list, count);
   if (limit > 0)
     e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
-                c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
-                (const uint32_t*)list, (const uint32_t*)count, limit);
+                c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), G, c->oslots.as<uint32_t>(),
+                c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
+                limit);
   const uint32_t wide = ceil_div(nblk, kWave) < kWideGrid ? ceil_div(nblk, kWave) : kWideGrid;
   e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(wide), dim3(kWave), s,
-              c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), c->slots.as<uint32_t>(), c->sizes.as<uint8_t>(),
-              (const uint32_t*)list, (const uint32_t*)count, limit);
+              c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
+              c->oslots.as<uint32_t>(), c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list,
+              (const uint32_t*)count, limit);
   return e;
 }
 
@@ -358,8 +367,6 @@ int launch_huff_encode(myyuv_hip_ctx* c, uint32_t nblk, uint32_t nf, hipStream_t
 int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void* d_out,
                     uint32_t cap, uint32_t* d_size, hipStream_t s) {
   const uint32_t nf = G.nframes;
-  const uint32_t nblk = G.cum[3];
-  const uint32_t ntiles = ceil_div(nblk, kScanTile);
   const QTables* qt = c->qtd.as<const QTables>();
   unsigned long long* err = c->err.as<unsigned long long>();
   int e = 0;
@@ -368,20 +375,13 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
               c->sink.as<uint4>(), c->work.as<uint32_t>());
   if ((c->skip >> MYYUV_K_FDCT) & 1u)  // diagnostic skip: keep K1's reset of the overflow count
     e |= hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess;
-  e |= launch_huff_encode(c, nblk * nf, nf, s);
-  ScanSrc S;
-  for (int i = 0; i < 4; i++) S.cum[i] = G.cum[i];
-  for (int p = 0; p < 3; p++) S.pos[p] = G.cum[p];
-  e |= launch(c, MYYUV_K_SCAN, k_scan_chain, dim3(ntiles, nf), dim3(256), s,
-              c->sizes.as<const uint8_t>(), nblk, S, (const uint32_t*)nullptr, 0u, G,
-              (StreamDesc*)nullptr, c->loff.as<uint32_t>(), c->tiles.as<uint32_t>(), ntiles,
-              c->status.as<unsigned long long>(), next_epoch(c), err);
-  const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], 256), t1 = ceil_div(G.cum[2] - G.cum[1], 256),
-                 t2 = ceil_div(G.cum[3] - G.cum[2], 256);
-  e |= launch(c, MYYUV_K_COMPACT, k_compact, dim3(t0 + t1 + t2, nf), dim3(256), s,
-              c->slots.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
-              c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
+  e |= launch_huff_encode(c, G, s);
+  e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(1024), s, c->tinfo.as<uint32_t>(), G,
               static_cast<uint8_t*>(d_out), cap, d_size, err);
+  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
+              c->stage.as<const uint32_t>(), c->tinfo.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
+              c->srcoff.as<const uint16_t>(), c->oslots.as<const uint32_t>(), G, static_cast<uint8_t*>(d_out),
+              cap);
   return e ? MYYUV_E_HIP : 0;
 }
 
@@ -543,7 +543,7 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->done);
-  DevBuf* bufs[] = {&c->frame, &c->coef, &c->slots, &c->sizes, &c->loff,  &c->tiles, &c->payload,
+  DevBuf* bufs[] = {&c->frame, &c->coef, &c->stage, &c->oslots, &c->tinfo, &c->srcoff, &c->sizes, &c->loff, &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
                     &c->bmp,   &c->rmask, &c->zq, &c->bsizes};
   for (auto* b : bufs) b->release();
@@ -1004,7 +1004,8 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   StreamOrder so(c, s);
   FrameGeom G;
   std::memset(&G, 0, sizeof(G));
-  G.cum[1] = G.cum[2] = G.cum[3] = nblocks;
+  G.cum[1] = G.cum[2] = G.cum[3] = nblocks;  // one plane of nblocks blocks
+  G.tcum[1] = G.tcum[2] = G.tcum[3] = ceil_div(nblocks, kK2Group);
   G.nframes = 1;
   if (reserve(c, G)) return MYYUV_E_HIP;
   const uint32_t nwaves = ceil_div(nblocks, kWave);
@@ -1020,22 +1021,24 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
       hipMemsetAsync(c->rmask.p, 0xFF, nblocks, s) != hipSuccess ||  // every row present
       hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess)  // K1 zeroes it in the codec path
     return MYYUV_E_HIP;
-  if (launch_huff_encode(c, nblocks, 1, s)) return MYYUV_E_HIP;
-  std::vector<uint32_t> slots((size_t)nwaves * kSlotWords * kWave);
-  if (hipMemcpyAsync(slots.data(), c->slots.p, slots.size() * 4, hipMemcpyDeviceToHost, s) !=
-          hipSuccess ||
+  if (launch_huff_encode(c, G, s)) return MYYUV_E_HIP;
+  // K2's hand-off (codec_common.hpp): per tile the waves' dense runs, the
+  // chunks of blocks with more than 8 symbols in their own slots
+  const uint32_t ntile = G.tcum[3];
+  std::vector<uint8_t> stage((size_t)ntile * kTileCap), oslots((size_t)nblocks * kMaxChunk);
+  std::vector<uint16_t> soff(nblocks);
+  if (hipMemcpyAsync(stage.data(), c->stage.p, stage.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(oslots.data(), c->oslots.p, oslots.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(soff.data(), c->srcoff.p, (size_t)nblocks * 2, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipMemcpyAsync(sizes, c->sizes.p, nblocks, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return MYYUV_E_HIP;
-  for (uint32_t b = 0; b < nblocks; b++) {
-    const uint32_t* base = slots.data() + (size_t)(b / kWave) * kSlotWords * kWave + (b % kWave);
-    uint8_t* dst = chunks160 + (size_t)b * kMaxChunk;
+  for (uint32_t g = 0; g < nblocks; g++) {
+    uint8_t* dst = chunks160 + (size_t)g * kMaxChunk;
     std::memset(dst, 0, kMaxChunk);
-    const uint32_t nw = (sizes[b] + 3u) / 4u;
-    for (uint32_t j = 0; j < nw && j < (uint32_t)kSlotWords; j++) {
-      const uint32_t v = base[(size_t)j * kWave];
-      std::memcpy(dst + 4 * j, &v, 4);
-    }
+    const uint8_t* src = soff[g] == kSrcOverflow ? oslots.data() + (size_t)g * kMaxChunk
+                                                 : stage.data() + (size_t)(g / kK2Group) * kTileCap + soff[g];
+    std::memcpy(dst, src, sizes[g]);
   }
   return 0;
 }
