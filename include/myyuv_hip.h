@@ -161,7 +161,7 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
 #define MYYUV_K_HUFF_ENC 1   /* K2 huff_encode (CAP=8 pass over every block) */
 #define MYYUV_K_SCAN 2       /* single-pass chunk-size scan (both directions; decode: + header checks) */
 #define MYYUV_K_COMPACT 3    /* K4 stream writer: look-back scan + tiles into the DCTYUV stream */
-#define MYYUV_K_PARSE 4      /* (unused: the header checks run inside MYYUV_K_SCAN) */
+#define MYYUV_K_ENCODE_TILE 4 /* fused single-pass encoder K1 + K2 (MYYUV_ENCODER=fused) */
 #define MYYUV_K_HUFF_DEC 5   /* K5 huff_decode */
 #define MYYUV_K_IDCT 6       /* K6 dequant_idct */
 #define MYYUV_K_HUFF_WIDE 7  /* K2 overflow pass, lane per block (long worklists) */

@@ -33,11 +33,22 @@ def oracle():
     return O
 
 
-@pytest.fixture(scope="session")
-def codec():
+@pytest.fixture(scope="session", params=["split", "fused"])
+def codec(request):
+    """A codec context per encoder: K1 -> K2 through HBM ("split") and the
+    fused single-pass encoder k_encode_tile ("fused"; MYYUV_ENCODER is read
+    when the context is created).  Every test taking `codec` runs on both."""
     import myyuv_hip
 
-    c = myyuv_hip.Codec(0)
+    old = os.environ.get("MYYUV_ENCODER")
+    os.environ["MYYUV_ENCODER"] = request.param
+    try:
+        c = myyuv_hip.Codec(0)
+    finally:
+        if old is None:
+            del os.environ["MYYUV_ENCODER"]
+        else:
+            os.environ["MYYUV_ENCODER"] = old
     yield c
     c.close()
 

@@ -203,3 +203,30 @@ def test_python_compress_batch_checks_frame_sizes(codec):
     raw = open(SMALL, "rb").read()[64:]
     with pytest.raises(ValueError, match="frame 1"):
         codec.compress_batch([raw, raw[:-1]], 992, 736, (50, 50, 50))
+
+
+@pytest.mark.gpu
+def test_cli_batch_compress_over_devices(tmp_path, oracle):
+    """-batch-compress -devices 0,0,0: frames dealt round-robin over three
+    host threads with a codec context each (the C++ side of the
+    frame-per-GPU sharding; one physical GPU here, so the three
+    entries name the same device); every output equals the per-file result."""
+    import numpy as np
+    import myyuv_file
+    rng = np.random.default_rng(9)
+    files = []
+    for i in range(7):  # mixed geometries, uneven shares (3, 2, 2)
+        w, h = (128, 64) if i % 2 else (256, 128)
+        raw = rng.integers(0, 256, w * h * 3 // 2).astype(np.uint8).tobytes()
+        p = tmp_path / f"f{i}.myyuv"
+        myyuv_file.YUVFile(width=w, height=h, data=raw).dump(str(p))
+        files.append(p)
+    out = tmp_path / "out"
+    out.mkdir()
+    r = run(CLI, "-batch-compress", "DCT", "60", "-devices", "0,0,0", "-o", str(out), *map(str, files))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "(7 frames)" in r.stdout
+    for p in files:
+        f = myyuv_file.YUVFile.load(str(p))
+        want = f.compressed(bytes([60] * 3), oracle.compress(f.data, f.width, f.height, (60, 60, 60))).dumps()
+        assert (out / p.name).read_bytes() == want, p.name

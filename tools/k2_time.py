@@ -39,7 +39,17 @@ def run(raw, w, h, q, label, iters=10):
     import numpy as np
     fs = np.zeros(8192 * 8, np.uint32)
     L.myyuv_debug_k2_fstamps(fs.ctypes.data_as(ctypes.c_void_p), 8192)
-    fs = fs.reshape(-1, 8)[:, 1:6]
+    fs8 = fs.reshape(-1, 8)
+    cls_names = {0: 'single', 1: 'r4', 2: 'r8'}
+    used = fs8[:, 7] > 0
+    for cl in (0, 1, 2):
+        sel = used & ((fs8[:, 0] & 0xFF) == cl)
+        if sel.any():
+            st = fs8[sel]
+            stages = {names[k]: int(st[:, k].mean()) for k in range(1, 5)}
+            print(f"   class {cls_names[cl]:6s}: {sel.sum():5d} waves, wave msz mean {(st[:, 0] >> 8).mean():5.1f}, "
+                  f"total cycles mean {st[:, 7].mean():8.0f}, build stages {stages}", flush=True)
+    fs = fs8[:, 1:6]
     fs = fs[fs.sum(1) > 0]
     fast = {names[k + 1]: int(fs[:, k].mean()) for k in range(5)}
     fast_max = {names[k + 1]: int(fs[:, k].max()) for k in range(5)}

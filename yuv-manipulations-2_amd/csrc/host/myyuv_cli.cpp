@@ -11,7 +11,8 @@
 //   myyuv_cli in.bmp -to_yuv IYUV -o out.myyuv   (conversion on the GPU, K7)
 // and, beyond the reference CLI, many frames per invocation (SURVEY.md §8f
 // row 2; frames of one geometry share batched kernel launches):
-//   myyuv_cli -batch-compress DCT Q [Q [Q]] -o OUTDIR IN.myyuv...
+//   myyuv_cli -batch-compress DCT Q [Q [Q]] [-devices D0,D1,...] -o OUTDIR IN.myyuv...
+//     (-devices: frames dealt round-robin over those GPUs, one host thread each)
 //   myyuv_cli -batch-decompress -o OUTDIR IN.myyuv...
 // each output is OUTDIR/<input file name>, byte-identical to the per-file
 // command's.
@@ -43,7 +44,7 @@ void usage() {
             << "  myyuv_cli IMAGE.myyuv -decompress -o OUT.myyuv\n"
             << "  myyuv_cli IMAGE.bmp -info\n"
             << "  myyuv_cli IMAGE.bmp -to_yuv IYUV -o OUT.myyuv\n"
-            << "  myyuv_cli -batch-compress DCT Q [Q [Q]] -o OUTDIR IMAGE.myyuv...\n"
+            << "  myyuv_cli -batch-compress DCT Q [Q [Q]] [-devices D0,D1,...] -o OUTDIR IMAGE.myyuv...\n"
             << "  myyuv_cli -batch-decompress -o OUTDIR IMAGE.myyuv...\n"
             << "\nYUV formats:\nIYUV\n\nCompression formats for YUV:\nDCT\n"
             << "\nExample:\n  myyuv_cli image.myyuv -compress DCT 50 -o image-DCT-50.myyuv\n";
@@ -176,11 +177,25 @@ int run_batch(const std::vector<std::string>& args) {
   const bool comp = args[1] == "-batch-compress";
   size_t a = 2;
   std::vector<std::string> params;
+  std::vector<int> devices;
   if (comp) {
     if (a >= args.size() || args[a] != "DCT")
       throw std::runtime_error("Compression not registered: " + (a < args.size() ? args[a] : std::string()));
     a++;
-    while (a < args.size() && args[a] != "-o") params.push_back(args[a++]);
+    while (a < args.size() && args[a] != "-o") {
+      if (args[a] == "-devices" && a + 1 < args.size()) {  // frames dealt round-robin over these GPUs
+        std::string list = args[a + 1];
+        for (size_t k = 0; k <= list.size();) {
+          const size_t e = list.find(',', k);
+          devices.push_back(std::stoi(list.substr(k, e == std::string::npos ? std::string::npos : e - k)));
+          if (e == std::string::npos) break;
+          k = e + 1;
+        }
+        a += 2;
+        continue;
+      }
+      params.push_back(args[a++]);
+    }
   }
   if (a + 2 >= args.size() || args[a] != "-o") {
     std::cout << "Invalid arguments. Expected -o OUTDIR followed by input files\n";
@@ -214,7 +229,7 @@ int run_batch(const std::vector<std::string>& args) {
       }
       std::vector<const myyuv::YUV*> ptrs;
       for (const auto& y : in) ptrs.push_back(&y);
-      out = myyuvDCT::compress_DCT_planar_batch(ptrs, {q[0], q[1], q[2]});
+      out = myyuvDCT::compress_DCT_planar_batch(ptrs, {q[0], q[1], q[2]}, devices);
     } else {
       for (const auto& y : in) out.push_back(y.decompress());
     }

@@ -12,6 +12,9 @@
 #include <stdexcept>
 #include <vector>
 
+#include <exception>
+#include <thread>
+
 #include "myyuv_hip.h"
 
 namespace {
@@ -325,37 +328,33 @@ myyuv::YUV compress_DCT_planar(const myyuv::YUV& yuv, const std::array<uint8_t, 
   return res;
 }
 
-std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames,
-                                                  const std::array<uint8_t, 3>& params) {
+namespace {
+
+// Frames `idx` of `frames` (any geometries) on context h: frames of one
+// geometry share one batched launch of every kernel (up to kMaxBatch).
+void compress_share(myyuv_hip_handle h, const std::vector<const myyuv::YUV*>& frames,
+                    const std::vector<size_t>& idx, const std::array<uint8_t, 3>& params,
+                    std::vector<myyuv::YUV>& out) {
   using myyuv::YUV;
-  for (uint8_t q : params)
-    if (q < 1 || q > 100) throw std::runtime_error("Level of quality must be between 1 and 100");
-  for (const YUV* y : frames) {
-    if (y->getFormatGroup() != YUV::FormatGroup::PLANAR)
-      throw std::runtime_error("Error compressing: YUV must be planar");
-    if (y->getCompression() != YUV::Compressions::NONE)
-      throw std::runtime_error("Error compressing: can't compress uncompressed YUV");
-  }
-  std::vector<YUV> out(frames.size());
-  std::vector<bool> done(frames.size(), false);
+  std::vector<bool> done(idx.size(), false);
   constexpr size_t kMaxBatch = 16;  // frames per batched launch
-  for (size_t i = 0; i < frames.size(); i++) {
+  for (size_t i = 0; i < idx.size(); i++) {
     if (done[i]) continue;
-    const uint32_t w = frames[i]->header.width, h = frames[i]->header.height;
-    std::vector<size_t> group;  // this geometry, in input order
-    for (size_t j = i; j < frames.size() && group.size() < kMaxBatch; j++)
-      if (!done[j] && frames[j]->header.width == w && frames[j]->header.height == h) group.push_back(j);
-    const size_t fbytes = (size_t)w * h * 3 / 2;
-    const uint32_t cap = (myyuv_dct_payload_bound(w, h) + 3u) & ~3u;
+    const uint32_t w = frames[idx[i]]->header.width, hh = frames[idx[i]]->header.height;
+    std::vector<size_t> group;  // positions in idx of this geometry, in input order
+    for (size_t j = i; j < idx.size() && group.size() < kMaxBatch; j++)
+      if (!done[j] && frames[idx[j]]->header.width == w && frames[idx[j]]->header.height == hh) group.push_back(j);
+    const size_t fbytes = (size_t)w * hh * 3 / 2;
+    const uint32_t cap = (myyuv_dct_payload_bound(w, hh) + 3u) & ~3u;
     std::vector<uint8_t> in(fbytes * group.size()), pay((size_t)cap * group.size());
     std::vector<uint32_t> sizes(group.size());
-    for (size_t k = 0; k < group.size(); k++) std::memcpy(in.data() + k * fbytes, frames[group[k]]->data, fbytes);
-    const int rc = myyuv_gpu_dct_compress_batch(t_codec.get(), in.data(), (uint32_t)group.size(), w, h,
-                                                params.data(), pay.data(), cap, sizes.data());
+    for (size_t k = 0; k < group.size(); k++) std::memcpy(in.data() + k * fbytes, frames[idx[group[k]]]->data, fbytes);
+    const int rc = myyuv_gpu_dct_compress_batch(h, in.data(), (uint32_t)group.size(), w, hh, params.data(),
+                                                pay.data(), cap, sizes.data());
     if (rc) fail(rc);
     for (size_t k = 0; k < group.size(); k++) {
-      const YUV& src = *frames[group[k]];
-      YUV& res = out[group[k]];
+      const YUV& src = *frames[idx[group[k]]];
+      YUV& res = out[idx[group[k]]];
       res.header = src.header;  // header rewrite as compress_DCT_planar (DCT.cpp:389-396)
       res.header.compression = YUV::Compressions::DCT;
       res.header.compression_params_size = 3;
@@ -368,6 +367,62 @@ std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv:
       done[group[k]] = true;
     }
   }
+}
+
+void check_compressible(const std::vector<const myyuv::YUV*>& frames, const std::array<uint8_t, 3>& params) {
+  using myyuv::YUV;
+  for (uint8_t q : params)
+    if (q < 1 || q > 100) throw std::runtime_error("Level of quality must be between 1 and 100");
+  for (const YUV* y : frames) {
+    if (y->getFormatGroup() != YUV::FormatGroup::PLANAR)
+      throw std::runtime_error("Error compressing: YUV must be planar");
+    if (y->getCompression() != YUV::Compressions::NONE)
+      throw std::runtime_error("Error compressing: can't compress uncompressed YUV");
+  }
+}
+
+}  // namespace
+
+std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames,
+                                                  const std::array<uint8_t, 3>& params) {
+  check_compressible(frames, params);
+  std::vector<myyuv::YUV> out(frames.size());
+  std::vector<size_t> all(frames.size());
+  for (size_t i = 0; i < frames.size(); i++) all[i] = i;
+  compress_share(t_codec.get(), frames, all, params, out);
+  return out;
+}
+
+// Frames dealt round-robin over `devices` (frame i -> devices[i % n], the
+// multi-GPU sharding of SURVEY.md §8e), one host thread and codec context per
+// entry; results in input order.  The first failure is rethrown.
+std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames,
+                                                  const std::array<uint8_t, 3>& params,
+                                                  const std::vector<int>& devices) {
+  if (devices.empty()) return compress_DCT_planar_batch(frames, params);
+  check_compressible(frames, params);
+  std::vector<myyuv::YUV> out(frames.size());
+  const size_t n = devices.size();
+  std::vector<std::exception_ptr> errs(n);
+  std::vector<std::thread> th;
+  for (size_t d = 0; d < n; d++) {
+    th.emplace_back([&, d] {
+      myyuv_hip_handle h = nullptr;
+      try {
+        const int rc = myyuv_hip_create(devices[d], &h);
+        if (rc) fail(rc);
+        std::vector<size_t> mine;
+        for (size_t i = d; i < frames.size(); i += n) mine.push_back(i);
+        compress_share(h, frames, mine, params, out);
+      } catch (...) {
+        errs[d] = std::current_exception();
+      }
+      if (h) myyuv_hip_destroy(h);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
   return out;
 }
 

@@ -110,4 +110,10 @@ myyuv::YUV decompress_DCT_planar(const myyuv::YUV& yuv, const std::array<uint8_t
 // one batched launch of every kernel; result i is compress_DCT_planar(*frames[i]).
 std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames,
                                                   const std::array<uint8_t, 3>& params);
+// The same over several devices: frame i on devices[i % n] (frames sharded
+// one per GPU round-robin), one host thread and context per
+// entry (an id may repeat: several contexts on one device).
+std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames,
+                                                  const std::array<uint8_t, 3>& params,
+                                                  const std::vector<int>& devices);
 }  // namespace myyuvDCT

@@ -60,6 +60,7 @@ extern __device__ uint32_t g_k2_fstamps[8192 * 8];
   } while (0)
 #endif
 #include "huff_common.hpp"
+#include "xform_common.hpp"
 
 namespace myyuv_gpu {
 
@@ -740,44 +741,83 @@ __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict
   }
 }
 
-// Fast pass over every block, one workgroup per tile (kK2Group consecutive
-// blocks of one plane of one frame: FrameGeom::tcum; grid (tiles, frames)).
-// The workgroup classifies its blocks (block_class: one symbol / <= 4 / <= 8
-// distinct for sure / the rest), sorts them by class through LDS and hands
-// each wave 64 blocks of (nearly) one class, so a wave runs the cheapest
-// register-resident encoder that fits all its blocks and its loops run to the
-// maxima of similar blocks rather than of a 64-block stretch of the frame.
-// Sorted chunks are dealt to the waves so that each SIMD gets one heavy and
-// one light chunk.  Each lane builds its block's code (sizes known before a
-// bit is written), a wave scan gives every chunk its byte offset, and the
-// wave's chunks go back to back into its dense run (DenseWriter: every dword
-// stored once, by the block owning its first byte); srcoff records where
-// each block's chunk is (codec_common.hpp, K2 -> K4).  Blocks with more than
-// 8 distinct symbols are appended to `work` for the overflow passes.
-//   coef: natural-order quads (codec_common.hpp); sizes: [n] u8.
-#ifndef MYYUV_K2_WAVES
-#define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (a few spills; +2.6 % in the bench, tools/ab_bench.sh)
-#endif
-__global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
-                                                         const uint8_t* __restrict__ rmask,
-                                                         const uint4* __restrict__ zq, FrameGeom G,
-                                                         uint32_t* __restrict__ stage,
-                                                         uint32_t* __restrict__ tinfo,
-                                                         uint8_t* __restrict__ sizes,
-                                                         uint16_t* __restrict__ srcoff,
-                                                         uint32_t* __restrict__ work,
-                                                         uint32_t* __restrict__ work_count) {
-  constexpr int kWaves = kK2Group / kWave;
-  __shared__ uint32_t s_g[kK2Group];  // sorted position -> the tile's block
-  __shared__ uint8_t s_msz[kK2Group], s_cls[kK2Group], s_rm[kK2Group];
-  __shared__ uint32_t s_cnt[kWaves][kClassDead + 1];
+namespace {
+
+// Coefficient sources of encode_tile: K1's quads in HBM (k_huff_encode), or
+// the tile's LDS image (k_encode_tile: row c of the tile's block b at
+// c * kK2Group + b), which also hands the overflow blocks' coefficients to the
+// overflow passes through HBM.
+struct GlobalCoef {
+  const uint4* coef;
+  const uint8_t* rmask;
+  const uint4* zq;
+  uint32_t gb;  // batch-global index of the tile's block 0
+  __device__ __forceinline__ uint32_t rm(uint32_t b) const { return rmask[gb + b]; }
+  __device__ __forceinline__ void load(CoefRegs& R, uint32_t b, uint32_t m) const { R.load(coef, zq, gb + b, m); }
+  __device__ __forceinline__ void spill(const CoefRegs&, uint32_t, uint32_t) const {}
+};
+
+template <bool kSpill>
+struct LdsCoefT {
+  const uint4* img;
+  const uint8_t* s_rm;
+  uint4* coef;
+  uint8_t* rmask;
+  uint32_t gb;
+  __device__ __forceinline__ uint32_t rm(uint32_t b) const { return s_rm[b]; }
+  __device__ __forceinline__ void load(CoefRegs& R, uint32_t b, uint32_t m) const {
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint4 v = (m >> c) & 1u ? img[c * kK2Group + b] : make_uint4(0, 0, 0, 0);
+      R.w[4 * c] = v.x;
+      R.w[4 * c + 1] = v.y;
+      R.w[4 * c + 2] = v.z;
+      R.w[4 * c + 3] = v.w;
+    }
+  }
+  // a block for the overflow passes: its nonzero rows and row mask to HBM (K1's layout)
+  __device__ __forceinline__ void spill(const CoefRegs& R, uint32_t b, uint32_t m) const {
+    if (!kSpill) return;
+    const uint32_t g = gb + b;
+#pragma unroll
+    for (int c = 0; c < 8; c++)
+      if ((m >> c) & 1u) coef[coef_quad(g, c)] = make_uint4(R.w[4 * c], R.w[4 * c + 1], R.w[4 * c + 2], R.w[4 * c + 3]);
+    rmask[g] = (uint8_t)m;
+  }
+};
+
+using LdsCoef = LdsCoefT<true>;
+constexpr int kTileWaves = kK2Group / kWave;
+
+// K2's scratch in LDS (k_encode_tile lays it over its transpose tiles).
+struct TileScratch {
+  uint32_t g[kK2Group];  // sorted position -> the tile's block
+  uint8_t msz[kK2Group], cls[kK2Group], rm[kK2Group];
+  uint32_t cnt[kTileWaves][kClassDead + 1];
+};
+
+// K2 on one tile (kK2Group consecutive blocks of one plane of one frame:
+// FrameGeom::tcum; workgroup = kK2Group threads).  The workgroup classifies
+// its blocks (block_class: one symbol / <= 4 / <= 8 distinct for sure / the
+// rest), sorts them by class through LDS and hands each wave 64 blocks of
+// (nearly) one class, so a wave runs the cheapest register-resident encoder
+// that fits all its blocks and its loops run to the maxima of similar blocks
+// rather than of a 64-block stretch of the frame.  Sorted chunks are dealt to
+// the waves so that each SIMD gets one heavy and one light chunk.  Each lane
+// builds its block's code (sizes known before a bit is written), a wave scan
+// gives every chunk its byte offset, and the wave's chunks go back to back
+// into its dense run (DenseWriter: every dword stored once, by the block
+// owning its first byte); srcoff records where each block's chunk is
+// (codec_common.hpp, K2 -> K4).  Blocks with more than 8 distinct symbols are
+// appended to `work` for the overflow passes.
+template <class Src>
+__device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uint32_t T, uint32_t nloc,
+                                            uint32_t* __restrict__ stage, uint32_t* __restrict__ tinfo,
+                                            uint8_t* __restrict__ sizes, uint16_t* __restrict__ srcoff,
+                                            uint32_t* __restrict__ work, uint32_t* __restrict__ work_count) {
+  constexpr int kWaves = kTileWaves;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t t = blockIdx.x, f = blockIdx.y;
-  const uint32_t T = f * G.tcum[3] + t;  // batch tile
-  const int p = tile_plane(G, t);
-  const uint32_t g0 = tile_first(G, p, t);
-  const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
-  const uint32_t gb = f * G.cum[3] + g0;  // batch-global index of the tile's block 0
+  const uint32_t gb = src.gb;
   // the overflow passes add their chunk bytes to the tile's info word 0
   // (ordered before them by the kernel boundary)
   if (tid == 0) tinfo[(size_t)T * kTInfoWords] = 0u;
@@ -786,9 +826,9 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   int msz = 0;
   uint32_t rm = 0;
   if (tid < nloc) {
-    rm = rmask[gb + tid];
+    rm = src.rm(tid);
     CoefRegs R;
-    R.load(coef, zq, gb + tid, rm);
+    src.load(R, tid, rm);
     msz = R.msz();
     cls = block_class(R, msz);
   }
@@ -799,7 +839,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   for (uint32_t c = 0; c <= kClassDead; c++) {
     const uint64_t b = __ballot(cls == c);
     if (cls == c) rank = (uint32_t)__popcll(b & below);
-    if (lane == 0) s_cnt[wave][c] = (uint32_t)__popcll(b);
+    if (lane == 0) sc.cnt[wave][c] = (uint32_t)__popcll(b);
   }
   __syncthreads();
   uint32_t pos = rank;
@@ -807,18 +847,19 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   for (uint32_t c = 0; c <= kClassDead; c++)
 #pragma unroll
     for (uint32_t w = 0; w < (uint32_t)kWaves; w++)
-      pos += (c < cls || (c == cls && w < wave)) ? s_cnt[w][c] : 0u;
-  s_g[pos] = tid;
-  s_msz[pos] = (uint8_t)msz;
-  s_cls[pos] = (uint8_t)cls;
-  s_rm[pos] = (uint8_t)rm;
+      pos += (c < cls || (c == cls && w < wave)) ? sc.cnt[w][c] : 0u;
+  sc.g[pos] = tid;
+  sc.msz[pos] = (uint8_t)msz;
+  sc.cls[pos] = (uint8_t)cls;
+  sc.rm[pos] = (uint8_t)rm;
   __syncthreads();
   // ---- build: wave w takes sorted chunk w < kWaves/2 ? kWaves-1-w : w-kWaves/2
   const uint32_t chunk = wave < (uint32_t)kWaves / 2 ? kWaves - 1 - wave : wave - kWaves / 2;
   const uint32_t e = chunk * kWave + lane;
-  const uint32_t ml = s_g[e];  // the lane's block in the tile (every one of 0..255 once)
-  const int mm = s_msz[e];
-  const uint32_t mc = s_cls[e];
+  const uint32_t ml = sc.g[e];  // the lane's block in the tile (every one of 0..255 once)
+  const int mm = sc.msz[e];
+  const uint32_t mc = sc.cls[e];
+  const uint32_t mrm = sc.rm[e];
   const bool live = mc != kClassDead;
   const uint32_t mg = gb + ml;
   uint32_t wcls = kClassDead;  // the wave's heaviest live class
@@ -827,7 +868,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     if (wcls == kClassDead && __ballot(mc == (uint32_t)c) != 0) wcls = (uint32_t)c;
   const int wmsz = max(wave_max(live ? mm : 0), 1);
 #ifdef MYYUV_STAMPS
-  const uint32_t wid = (f * G.tcum[3] + t) * kWaves + wave;
+  const uint32_t wid = T * kWaves + wave;
   if (lane == 0 && wid < 8192) g_k2_fstamps[wid * 8 + 0] = wcls | ((uint32_t)wmsz << 8);
   const unsigned long long _w0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -835,7 +876,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   bool ok = false;
   if (wcls != kClassDead) {
     CoefRegs R;
-    R.load(coef, zq, live ? mg : gb, live ? s_rm[e] : 0u);
+    src.load(R, live ? ml : 0u, live ? mrm : 0u);
     if (wcls == kClassSingle) {
       if (live) {
         build_single(R, S);
@@ -846,6 +887,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     } else {
       if (live) ok = build_r<8>(R, mm, wmsz, S);
     }
+    if (live && !ok) src.spill(R, ml, mrm);
   }
   // ---- the wave's dense run: chunks back to back in the wave's order
   // (offsets by a wave scan of the sizes; no workgroup barrier), every dword
@@ -885,6 +927,148 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
 #ifdef MYYUV_STAMPS
   if (lane == 0 && wid < 8192) g_k2_fstamps[wid * 8 + 7] = (uint32_t)(__builtin_amdgcn_s_memtime() - _w0);
 #endif
+}
+
+}  // namespace
+
+// K2 over K1's coefficients in HBM: one workgroup per tile (grid (tiles, frames)).
+//   coef: natural-order quads (codec_common.hpp); sizes: [n] u8.
+#ifndef MYYUV_K2_WAVES
+#define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (a few spills; +2.6 % in the bench, tools/ab_bench.sh)
+#endif
+__global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
+                                                         const uint8_t* __restrict__ rmask,
+                                                         const uint4* __restrict__ zq, FrameGeom G,
+                                                         uint32_t* __restrict__ stage,
+                                                         uint32_t* __restrict__ tinfo,
+                                                         uint8_t* __restrict__ sizes,
+                                                         uint16_t* __restrict__ srcoff,
+                                                         uint32_t* __restrict__ work,
+                                                         uint32_t* __restrict__ work_count) {
+  __shared__ TileScratch sc;
+  const uint32_t t = blockIdx.x, f = blockIdx.y;
+  const int p = tile_plane(G, t);
+  const uint32_t g0 = tile_first(G, p, t);
+  const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
+  const GlobalCoef src{coef, rmask, zq, f * G.cum[3] + g0};
+  encode_tile(src, sc, f * G.tcum[3] + t, nloc, stage, tinfo, sizes, srcoff, work, work_count);
+}
+
+// Fused single-pass encoder: K1 + K2 for one tile, the
+// coefficients never leaving the chip.  Phase 1: wave w transforms the tile's
+// 16-block units 4w .. 4w+3 with K1's code (four lanes per block, all the
+// pixel rows loaded up front) into the tile's LDS coefficient image and row
+// masks.  Phase 2: encode_tile over that image; only blocks with more than 8
+// distinct symbols go to HBM, for the overflow passes.  LDS: 32 KB image +
+// 18 KB transpose tiles (K2's scratch is laid over them) + the Q tables:
+// three workgroups per CU.
+namespace {
+// K1's pixel rows 2q, 2q+1 of block b of units 4w .. 4w+3 of a tile (lanes
+// past the plane's end read its last block)
+struct TileRows {
+  uint4 px[4];
+};
+__device__ __forceinline__ void tile_geometry(const FrameGeom& G, uint32_t T, uint32_t& f, uint32_t& t, int& p,
+                                              uint32_t& g0, uint32_t& nloc) {
+  f = G.nframes > 1 ? T / G.tcum[3] : 0u;
+  t = T - f * G.tcum[3];
+  p = tile_plane(G, t);
+  g0 = tile_first(G, p, t);
+  nloc = min(kK2Group, G.cum[p + 1] - g0);
+}
+__device__ __forceinline__ xf::Unit plane_unit(const FrameGeom& G, int p) {
+  xf::Unit U;
+  U.p = p;
+  U.cum = G.cum[p];
+  U.nb = G.cum[p + 1] - G.cum[p];
+  U.poff = p == 0 ? G.poff[0] : (p == 1 ? G.poff[1] : G.poff[2]);
+  U.pw = p == 0 ? G.pw[0] : (p == 1 ? G.pw[1] : G.pw[2]);
+  U.bw = p == 0 ? G.bw[0] : (p == 1 ? G.bw[1] : G.bw[2]);
+  U.bmag = p == 0 ? G.bmag[0] : (p == 1 ? G.bmag[1] : G.bmag[2]);
+  U.local0 = 0;
+  return U;
+}
+__device__ __forceinline__ void load_tile_rows(const uint8_t* __restrict__ frame, const FrameGeom& G, uint32_t T,
+                                               uint32_t wave, uint32_t b, uint32_t q, TileRows& r) {
+  uint32_t f, t, g0, nloc;
+  int p;
+  tile_geometry(G, T, f, t, p, g0, nloc);
+  const xf::Unit U = plane_unit(G, p);
+  const uint32_t lbase = g0 - G.cum[p];
+  const uint8_t* fr = frame + (size_t)f * G.fbytes;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t local = lbase + (4 * wave + i) * kXfUnit + b;
+    const uint32_t off = xf::block_row_offset(U, local < U.nb ? local : U.nb - 1, 2u * q);
+    const uint2 r0 = *reinterpret_cast<const uint2*>(fr + off);
+    const uint2 r1 = *reinterpret_cast<const uint2*>(fr + off + U.pw);
+    r.px[i] = make_uint4(r0.x, r0.y, r1.x, r1.y);
+  }
+}
+}  // namespace
+
+// Fused single-pass encoder: K1 + K2 per tile, the
+// coefficients never leaving the chip; one workgroup per tile (grid (tiles,
+// frames)).  Phase 1: wave w transforms the tile's 16-block units 4w .. 4w+3
+// with K1's code (four lanes per block, all the pixel rows loaded up front)
+// into the tile's LDS coefficient image and row masks.  Phase 2: encode_tile
+// over that image; only blocks with more than 8 distinct symbols go to HBM,
+// for the overflow passes.  LDS: 32 KB image + 18 KB transpose tiles (K2's
+// scratch laid over them) + the Q tables: three workgroups per CU.
+// (A persistent variant prefetching the next tile's rows behind phase 2
+// measured slower: 250 against 209 us per 4-frame launch.)
+__global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __restrict__ frame, FrameGeom G,
+                                                             const QTables* __restrict__ qt,
+                                                             uint4* __restrict__ coef,
+                                                             uint8_t* __restrict__ rmask,
+                                                             uint32_t* __restrict__ stage,
+                                                             uint32_t* __restrict__ tinfo,
+                                                             uint8_t* __restrict__ sizes,
+                                                             uint16_t* __restrict__ srcoff,
+                                                             uint32_t* __restrict__ work,
+                                                             uint32_t* __restrict__ work_count) {
+  using namespace xf;
+  __shared__ uint4 s_img[8 * kK2Group];
+  __shared__ float s_tile[kTileWaves][kXfUnit * kTile];
+  __shared__ float s_q[2 * 3 * 64];
+  __shared__ uint8_t s_rmk[kK2Group];
+  static_assert(sizeof(TileScratch) <= sizeof(s_tile), "K2 scratch over the transpose tiles");
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t q = lane & 3u, b = lane >> 2;
+  const uint32_t T = blockIdx.y * G.tcum[3] + blockIdx.x;
+  uint32_t f, t, g0, nloc;
+  int p;
+  tile_geometry(G, T, f, t, p, g0, nloc);
+  TileRows rows;
+  load_tile_rows(frame, G, T, wave, b, q, rows);
+  stage_tables<2 * 3 * 64>(qt->q[0], s_q);
+  float* tb = s_tile[wave] + b * kTile;
+  uint8_t* img = reinterpret_cast<uint8_t*>(tb);
+  // ---- phase 1
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t lb = (4 * wave + i) * kXfUnit + b;
+    if ((4 * wave + i) * kXfUnit >= nloc) break;  // (wave-uniform) the tile's units end
+    *reinterpret_cast<uint2*>(img + 16u * q) = make_uint2(rows.px[i].x, rows.px[i].y);
+    *reinterpret_cast<uint2*>(img + 16u * q + 8u) = make_uint2(rows.px[i].z, rows.px[i].w);
+    wave_sync();
+    uint32_t c[16];
+    fdct_core(img, tb, q, s_q, p, c);
+    uint4 lo, hi;
+    uint32_t rm;
+    pack_quads(c, q, lo, hi, rm);
+    if (lb < nloc) {
+      s_img[(2 * q) * kK2Group + lb] = lo;
+      s_img[(2 * q + 1) * kK2Group + lb] = hi;
+      if (q == 0) s_rmk[lb] = (uint8_t)rm;
+    }
+    wave_sync();  // the tile is rewritten by the next unit
+  }
+  __syncthreads();
+  // ---- phase 2: K2 over the LDS image (its scratch over the transpose tiles)
+  TileScratch& sc = *reinterpret_cast<TileScratch*>(&s_tile[0][0]);
+  const LdsCoef src{s_img, s_rmk, coef, rmask, f * G.cum[3] + g0};
+  encode_tile(src, sc, T, nloc, stage, tinfo, sizes, srcoff, work, work_count);
 }
 
 // Overflow pass (CAP=64), lane per block, for long worklists (noise-like

@@ -145,38 +145,46 @@ __device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uin
 //     chunks in block order (applyDCTPlane's serial compaction, :314-322).
 // A frame has ~1.1k tiles (4032x3008): one workgroup scans them in a few
 // passes, so no look-back chain is needed anywhere.
-__global__ __launch_bounds__(1024) void k_tile_scan(uint32_t* __restrict__ tinfo, FrameGeom G,
-                                                   uint8_t* __restrict__ out, uint32_t cap,
-                                                   uint32_t* __restrict__ out_size,
-                                                   unsigned long long* __restrict__ err) {
-  __shared__ uint32_t s_w[16];
+__global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo, FrameGeom G,
+                                                  uint8_t* __restrict__ out, uint32_t cap,
+                                                  uint32_t* __restrict__ out_size,
+                                                  unsigned long long* __restrict__ err) {
+  // 256 threads (a small workgroup finds a free slot at once among the other
+  // launch groups' kernels): thread i scans tiles [i * per, (i + 1) * per)
+  __shared__ uint32_t s_w[4];
   __shared__ uint32_t s_carry;
   const uint32_t f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t ntile = G.tcum[3];
+  const uint32_t per = (ntile + 255) / 256;
   uint32_t* info = tinfo + (size_t)f * ntile * kTInfoWords;
-  if (tid == 0) s_carry = 0;
-  __syncthreads();
-  for (uint32_t base = 0; base < ntile; base += 1024) {
-    const uint32_t t = base + tid;
-    uint32_t v = 0;
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < per; k++) {
+    const uint32_t t = tid * per + k;
     if (t < ntile) {
       const uint32_t* w = info + (size_t)t * kTInfoWords;
-      v = w[0] + w[1] + w[2] + w[3] + w[4];
+      v += w[0] + w[1] + w[2] + w[3] + w[4];
     }
-    const uint32_t incl = wave_inclusive_scan(v);
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint32_t pre = s_carry, tot = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 16; k++) {
-      pre += k < wave ? s_w[k] : 0u;
-      tot += s_w[k];
-    }
-    if (t < ntile) info[(size_t)t * kTInfoWords + kTInfoPrefix] = pre + incl - v;
-    __syncthreads();
-    if (tid == 0) s_carry += tot;
-    __syncthreads();
   }
+  const uint32_t incl = wave_inclusive_scan(v);
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    pre += k < wave ? s_w[k] : 0u;
+    tot += s_w[k];
+  }
+  pre += incl - v;
+  for (uint32_t k = 0; k < per; k++) {
+    const uint32_t t = tid * per + k;
+    if (t < ntile) {
+      uint32_t* w = info + (size_t)t * kTInfoWords;
+      w[kTInfoPrefix] = pre;
+      pre += w[0] + w[1] + w[2] + w[3] + w[4];
+    }
+  }
+  if (tid == 0) s_carry = tot;
+  __syncthreads();
   // plane headers: the prefixes at the planes' first tiles (written above by
   // this workgroup; __syncthreads orders them)
   if (tid < 3) {

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -31,6 +32,8 @@ __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint
                                    const uint32_t*, const uint32_t*, uint32_t);
 __global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
                                    uint32_t*, const uint32_t*, const uint32_t*, uint32_t);
+__global__ void k_encode_tile(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint32_t*, uint32_t*,
+                              uint8_t*, uint16_t*, uint32_t*, uint32_t*);
 __global__ void k_tile_scan(uint32_t*, FrameGeom, uint8_t*, uint32_t, uint32_t*, unsigned long long*);
 __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
                              StreamDesc*, uint32_t*, uint32_t*, uint32_t, unsigned long long*,
@@ -174,6 +177,9 @@ struct myyuv_hip_ctx {
   DevBuf zq;    // 256 zero bytes: K6's source for rows the mask says are zero
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
+  // encoder: K1 -> K2 through HBM (split), or the fused single-pass kernel
+  // k_encode_tile (MYYUV_ENCODER=fused|split)
+  bool fused = false;
   // chained scan (k_chain.hpp): per-tile status words tagged with the launch
   // epoch, counted here
   DevBuf status;
@@ -339,16 +345,26 @@ uint32_t next_epoch(myyuv_hip_ctx* c) {
 // returns at once outside its regime.  A batch (nf > 1) takes the
 // lane-per-block pass only: its list is long, and the wave pass's per-block
 // SALU cost would crowd the other launch groups in flight (tools/kskip.py).
+int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s);
+
 int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
-  const uint32_t nf = G.nframes, nblk = G.cum[3] * nf;
+  const uint32_t nf = G.nframes;
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
+  const int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(G.tcum[3], nf), dim3(kK2Group), s,
+               c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
+               c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
+               c->srcoff.as<uint16_t>(), list, count);
+  return e | launch_overflow(c, G, s);
+}
+
+int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
+  const uint32_t nf = G.nframes, nblk = G.cum[3] * nf;
+  uint32_t* count = c->work.as<uint32_t>();
+  uint32_t* list = count + 64;
   const uint32_t limit = nf > 1 ? 0u : kWaveEncodeLimit;
-  int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(G.tcum[3], nf), dim3(kK2Group), s,
-                 c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
-                 c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
-                 c->srcoff.as<uint16_t>(), list, count);
+  int e = 0;
   if (limit > 0)
     e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
                 c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), G, c->oslots.as<uint32_t>(),
@@ -370,13 +386,24 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   const QTables* qt = c->qtd.as<const QTables>();
   unsigned long long* err = c->err.as<unsigned long long>();
   int e = 0;
-  e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
-              static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
-              c->sink.as<uint4>(), c->work.as<uint32_t>());
-  if ((c->skip >> MYYUV_K_FDCT) & 1u)  // diagnostic skip: keep K1's reset of the overflow count
-    e |= hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess;
-  e |= launch_huff_encode(c, G, s);
-  e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(1024), s, c->tinfo.as<uint32_t>(), G,
+  if (c->fused) {
+    // fused single-pass encoder (K1 + K2 per tile), then the overflow passes
+    uint32_t* count = c->work.as<uint32_t>();
+    e |= hipMemsetAsync(count, 0, 4, s) != hipSuccess;
+    e |= launch(c, MYYUV_K_ENCODE_TILE, k_encode_tile, dim3(G.tcum[3], nf), dim3(kK2Group), s,
+                static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
+                c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(), c->srcoff.as<uint16_t>(),
+                count + 64, count);
+    e |= launch_overflow(c, G, s);
+  } else {
+    e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
+                static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
+                c->sink.as<uint4>(), c->work.as<uint32_t>());
+    if ((c->skip >> MYYUV_K_FDCT) & 1u)  // diagnostic skip: keep K1's reset of the overflow count
+      e |= hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess;
+    e |= launch_huff_encode(c, G, s);
+  }
+  e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(256), s, c->tinfo.as<uint32_t>(), G,
               static_cast<uint8_t*>(d_out), cap, d_size, err);
   e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
               c->stage.as<const uint32_t>(), c->tinfo.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
@@ -522,6 +549,17 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
         cus > 0 && n1 > 0 && n6 > 0) {
       c->xf_resident[0] = (uint32_t)(cus * n1);
       c->xf_resident[1] = (uint32_t)(cus * n6);
+      {
+        const char* v = std::getenv("MYYUV_ENCODER");
+        c->fused = v && std::strcmp(v, "fused") == 0;
+      }
+      // tuning knobs (diagnostic; default 100): K1 / K6 grids as a percentage
+      // of the resident workgroups, leaving wave slots to other launch groups
+      for (int k = 0; k < 2; k++) {
+        const char* v = std::getenv(k == 0 ? "MYYUV_K1_GRID_PCT" : "MYYUV_K6_GRID_PCT");
+        const int pct = v ? std::atoi(v) : 100;
+        if (pct > 0 && pct < 100) c->xf_resident[k] = std::max(1u, c->xf_resident[k] * (uint32_t)pct / 100u);
+      }
     }
   }
   if (c->err.grow(8) || c->psize.grow(4) || c->desc.grow(sizeof(StreamDesc)) ||

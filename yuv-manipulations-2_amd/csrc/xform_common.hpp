@@ -1,0 +1,264 @@
+// xform_common.hpp — the 8x8 block transforms of K1 (fdct_quant) and K6
+// (dequant_idct), shared by k_transform.hip and the fused encoder
+// (k_huff_encode.hip, k_encode_tile).  See k_transform.hip for the design and
+// the bit-exactness argument (DCT.cpp:232-277, :325-335).
+#pragma once
+#include <stddef.h>
+
+#include "codec_common.hpp"
+
+namespace myyuv_gpu {
+namespace xf {
+
+constexpr float c_dct[64] = MYYUV_DCT_MATRIX;  // row u = basis u (DCT.cpp:221-230)
+constexpr int kTile = 72;  // floats per block in the transpose tile; (i, j) at tix(i, j)
+constexpr float kMagic = 0x1.8p23f;             // 1.5 * 2^23
+constexpr float kMagicPx = 0x1.8p23f + 128.0f;  // ... + 128: low byte = pixel
+constexpr float kHalfDown = 0x1.fffffep-2f;     // largest float below 0.5
+
+// Transpose tile: rows i = 2m, 2m+1 interleaved, so the pair a stage-2 lane
+// needs, (M[2q][k], M[2q+1][k]), is one 8-byte read; block stride 72 makes
+// those reads bank-conflict-free (the column-pair writes are 2-way).
+__device__ __forceinline__ constexpr int tix(int i, int j) { return (i >> 1) * 18 + 2 * j + (i & 1); }
+
+__device__ __forceinline__ uint32_t bits(float x) { return __builtin_bit_cast(uint32_t, x); }
+
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// Keeps 16 accumulators' updates in round-robin order (the scheduler would
+// otherwise serialise them chain by chain to save registers).
+__device__ __forceinline__ void fence16(float (&a)[16]) {
+  asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+               "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]),
+               "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15]));
+}
+
+// A 16-block unit of one plane, with the plane's geometry (wave-uniform;
+// selected from the kernel-argument fields by static index, so everything
+// stays in SGPRs with no scalar loads in the loop).
+struct Unit {
+  int p;            // plane
+  uint32_t local0;  // local index (inside the plane) of the unit's block 0
+  uint32_t nb;      // blocks in the plane
+  uint32_t cum;     // global index of the plane's block 0
+  uint32_t poff;    // byte offset of the plane in the frame
+  uint32_t pw;      // plane width (bytes per pixel row)
+  uint32_t bw;      // blocks per block-row
+  uint64_t bmag;    // FrameGeom::bmag of the plane
+};
+
+template <class T>
+__device__ __forceinline__ T pick(bool p1, bool p2, T a0, T a1, T a2) {
+  return p2 ? a2 : (p1 ? a1 : a0);
+}
+
+__device__ __forceinline__ Unit unit_of(const FrameGeom& G, uint32_t u) {
+  const bool p1 = u >= G.ucum[1], p2 = u >= G.ucum[2];
+  Unit r;
+  r.p = p2 ? 2 : (p1 ? 1 : 0);
+  r.local0 = (u - pick(p1, p2, G.ucum[0], G.ucum[1], G.ucum[2])) * kXfUnit;
+  r.cum = pick(p1, p2, G.cum[0], G.cum[1], G.cum[2]);
+  r.nb = pick(p1, p2, G.cum[1], G.cum[2], G.cum[3]) - r.cum;
+  r.poff = pick(p1, p2, G.poff[0], G.poff[1], G.poff[2]);
+  r.pw = pick(p1, p2, G.pw[0], G.pw[1], G.pw[2]);
+  r.bw = pick(p1, p2, G.bw[0], G.bw[1], G.bw[2]);
+  r.bmag = pick(p1, p2, G.bmag[0], G.bmag[1], G.bmag[2]);
+  return r;
+}
+
+// Byte offset in the frame of pixel row r of block `local` of the unit's
+// plane (block_row() with the plane's magic, codec_common.hpp).
+__device__ __forceinline__ uint32_t block_row_offset(const Unit& U, uint32_t local, uint32_t r) {
+  uint32_t by = local;
+  if (U.bmag != 0) {
+    const uint64_t lo = (uint64_t)local * (uint32_t)U.bmag;
+    const uint64_t hi = (uint64_t)local * (uint32_t)(U.bmag >> 32) + (lo >> 32);
+    by = (uint32_t)(hi >> 32);
+  }
+  const uint32_t bx = local - by * U.bw;
+  return U.poff + (by * 8u + r) * U.pw + bx * 8u;  // frames < 4 GiB
+}
+
+// The wave's first unit and stride (wave-uniform, in SGPRs).
+__device__ __forceinline__ uint32_t first_unit() {
+  return __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+}
+__device__ __forceinline__ uint32_t unit_stride() { return gridDim.x * 4u; }
+
+// Stage 2 of either transform for one lane's row pair: out[2v + h] =
+// sum_k P[2k + h] * B(v, k) (h = row 2q + h), k ascending, with
+// B(v, k) = D[v][k] (forward: T * D^T) or D[k][v] (inverse: U * D).
+// kSkip: a step k whose P[2k], P[2k+1] are zero in every lane of the wave is
+// skipped (the sums start at +0 and a +-0 product leaves a sum unchanged, so
+// the result is bit-identical; see K6).
+template <bool kInverse, bool kSkip = false>
+__device__ __forceinline__ void dot_rows(const float (&P)[16], float (&out)[16]) {
+  if (kSkip) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) out[j] = 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (kSkip && !__any(P[2 * k] != 0.0f || P[2 * k + 1] != 0.0f)) continue;
+    float pr[16];
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+      const float d = c_dct[kInverse ? k * 8 + v : v * 8 + k];
+      pr[2 * v] = P[2 * k] * d;
+      pr[2 * v + 1] = P[2 * k + 1] * d;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) out[j] = (k == 0 && !kSkip) ? pr[j] : out[j] + pr[j];
+    fence16(out);
+  }
+}
+
+// Column pairs (2q, 2q+1) of a block's 8x8 tile in the per-wave tile after
+// stage 1, read back as row pairs (2q, 2q+1): P[2k + h] = M[2q + h][k].
+__device__ __forceinline__ void transpose_tile(float* tb, uint32_t q, const float (&M)[16],
+                                               float (&P)[16]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    tb[tix(i, 2 * q)] = M[2 * i];
+    tb[tix(i, 2 * q + 1)] = M[2 * i + 1];
+  }
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float2 v = *reinterpret_cast<const float2*>(tb + tix(2 * q, k));
+    P[2 * k] = v.x;
+    P[2 * k + 1] = v.y;
+  }
+}
+
+__device__ __forceinline__ float sbyte(uint32_t w, int k) {  // byte k of w, sign-extended
+  return (float)(int)(int8_t)(uint8_t)(w >> (8 * k));
+}
+
+// Pixel rows 2q, 2q+1 of the lane's block in unit u (x/y: row 2q, z/w: row
+// 2q+1).  Lanes past the plane's end read the plane's last block (their
+// results go to the sink): the loads are unconditional and their values are
+// not touched until the next iteration, so the wave does not wait for them.
+__device__ __forceinline__ uint4 load_rows(const uint8_t* __restrict__ frame, const FrameGeom& G,
+                                           uint32_t ua, uint32_t b, uint32_t q) {
+  const uint32_t f = div_magic(ua, G.umag);
+  const Unit U = unit_of(G, ua - f * G.ucum[3]);
+  const uint32_t local = U.local0 + b;
+  const uint32_t off = block_row_offset(U, local < U.nb ? local : U.nb - 1, 2u * q);
+  const uint8_t* fr = frame + (size_t)f * G.fbytes;
+  const uint2 r0 = *reinterpret_cast<const uint2*>(fr + off);
+  const uint2 r1 = *reinterpret_cast<const uint2*>(fr + off + U.pw);
+  return make_uint4(r0.x, r0.y, r1.x, r1.y);
+}
+
+// The quality tables a kernel needs, staged once per workgroup into LDS.
+template <int kWords>
+__device__ __forceinline__ void stage_tables(const float* __restrict__ src, float* dst) {
+  static_assert(kWords <= 512, "two words per thread of the 256-thread workgroup");
+#pragma unroll
+  for (uint32_t i = threadIdx.x; i < 512u; i += 256u)
+    if (i < (uint32_t)kWords) dst[i] = src[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t unit_block(const FrameGeom& G, uint32_t ua, uint32_t b) {
+  const uint32_t f = div_magic(ua, G.umag);
+  const Unit U = unit_of(G, ua - f * G.ucum[3]);
+  const uint32_t local = U.local0 + b;
+  return f * G.cum[3] + U.cum + (local < U.nb ? local : U.nb - 1);
+}
+
+// Quads 2q, 2q+1 of block g; rows whose mask bit is clear read a zero quad
+// (always issued: unconditional loads keep the vmcnt pipelining)
+__device__ __forceinline__ void load_quads(const uint4* __restrict__ coef, const uint4* __restrict__ zq,
+                                           uint32_t g, uint32_t q, uint32_t m, uint4& a, uint4& c) {
+  const uint4* pa = (m >> (2 * q)) & 1u ? coef + coef_quad(g, 2 * q) : zq;
+  const uint4* pc = (m >> (2 * q + 1)) & 1u ? coef + coef_quad(g, 2 * q + 1) : zq;
+  a = *pa;
+  c = *pc;
+}
+
+
+// Forward transform + quantisation of lane (b, q)'s part of one block of a
+// 16-block unit (K1's per-unit body, DCT.cpp:269-277, :297-306): the block's
+// 8 pixel rows are in img (8 x 8 B, aliasing its transpose tile tb); out:
+// c[2v + h] holds, in its low 16 bits, the int16 coefficient of row 2q + h,
+// column v.  sqr: the Q tables then their reciprocals (QTables layout), p the
+// plane.
+__device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_t q, const float* sqr, int p,
+                                          uint32_t (&c)[16]) {
+  const uint32_t n0 = 16u * q;
+  // ---- columns 2q, 2q+1 of the block's 8 rows; x ^ 0x80 is x - 128 as a
+  // signed byte (DCT.cpp:303)
+  uint32_t xr[4];  // rows 2m (low half), 2m+1 (high half)
+#pragma unroll
+  for (int m = 0; m < 4; m++)
+    xr[m] = (*reinterpret_cast<const uint16_t*>(img + 16 * m + 2 * q) |
+             ((uint32_t)*reinterpret_cast<const uint16_t*>(img + 16 * m + 8 + 2 * q) << 16)) ^
+            0x80808080u;
+  wave_sync();
+  // ---- stage 1: T[i][j] = sum_k D[i][k] * X[k][j], j in {2q, 2q+1}
+  // (squareMatrixMul<8>(DCT, X), DCT.cpp:232-242); T[2i + c] = T[i][2q + c]
+  float T[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float x0 = sbyte(xr[k >> 1], 2 * (k & 1)), x1 = sbyte(xr[k >> 1], 2 * (k & 1) + 1);
+    float pr[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      pr[2 * i] = c_dct[i * 8 + k] * x0;
+      pr[2 * i + 1] = c_dct[i * 8 + k] * x1;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) T[j] = k == 0 ? pr[j] : T[j] + pr[j];
+    fence16(T);
+  }
+  // ---- transpose: columns (2q, 2q+1) in, rows (2q, 2q+1) out
+  float P[16];  // P[2k + h] = T[2q + h][k]
+  transpose_tile(tb, q, T, P);
+  // ---- stage 2: Y[i][v] = sum_k T[i][k] * D[v][k] (squareMatrixMulT<8>(T, DCT),
+  // DCT.cpp:244-254); coef = (int16)roundf(Y / Q) (DCT.cpp:273-276)
+  float Y[16];  // Y[2v + h] = Y[2q + h][v]
+  dot_rows<false>(P, Y);
+  // reciprocals of rows 2q, 2q+1 (natural n0 .. n0 + 15)
+  const float4* R4 = reinterpret_cast<const float4*>(sqr + 3 * 64 + p * 64 + n0);
+  const float4 r0 = R4[0], r1 = R4[1], r2 = R4[2], r3 = R4[3];
+  const float rr[16] = {r0.x, r2.x, r0.y, r2.y, r0.z, r2.z, r0.w, r2.w,
+                        r1.x, r3.x, r1.y, r3.y, r1.z, r3.z, r1.w, r3.w};  // [2v + h]
+  float mx = 0.0f;  // max over the lane of |e| + |t| * 2^-21: >= 0.5 near a tie
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const float tq = Y[j] * rr[j];
+    const float uu = tq + kMagic;
+    const float e = tq - (uu - kMagic);
+    mx = __builtin_fmaxf(mx, __builtin_fmaf(__builtin_fabsf(tq), kNearRel, __builtin_fabsf(e)));
+    c[j] = bits(uu);
+  }
+  if (mx >= 0.5f) {  // a near-tie in the lane: the reference's divide for all 16
+    const float* Qt = sqr + p * 64 + n0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) c[j] = (uint32_t)(int)roundf(Y[j] / Qt[(j >> 1) + 8 * (j & 1)]);
+  }
+}
+
+// Rows 2q, 2q+1 of the block as two coefficient quads (codec_common.hpp
+// layout) and the block's row mask (bit c: row c has a nonzero coefficient),
+// from its four lanes (lanes 4b .. 4b+3 of the wave).
+__device__ __forceinline__ void pack_quads(const uint32_t (&c)[16], uint32_t q, uint4& lo, uint4& hi,
+                                           uint32_t& rm) {
+  lo.x = __builtin_amdgcn_perm(c[2], c[0], 0x05040100u);
+  lo.y = __builtin_amdgcn_perm(c[6], c[4], 0x05040100u);
+  lo.z = __builtin_amdgcn_perm(c[10], c[8], 0x05040100u);
+  lo.w = __builtin_amdgcn_perm(c[14], c[12], 0x05040100u);
+  hi.x = __builtin_amdgcn_perm(c[3], c[1], 0x05040100u);
+  hi.y = __builtin_amdgcn_perm(c[7], c[5], 0x05040100u);
+  hi.z = __builtin_amdgcn_perm(c[11], c[9], 0x05040100u);
+  hi.w = __builtin_amdgcn_perm(c[15], c[13], 0x05040100u);
+  const bool nzl = (lo.x | lo.y | lo.z | lo.w) != 0u, nzh = (hi.x | hi.y | hi.z | hi.w) != 0u;
+  rm = (nzl ? 1u << (2 * q) : 0u) | (nzh ? 2u << (2 * q) : 0u);
+  rm |= __shfl_xor(rm, 1, 64);
+  rm |= __shfl_xor(rm, 2, 64);
+}
+
+}  // namespace xf
+}  // namespace myyuv_gpu
