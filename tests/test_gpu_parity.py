@@ -334,3 +334,28 @@ def test_batch_decode_error_reports_frame(codec, oracle, golden):
     rc, bad = codec.sync_status(stream)
     assert rc == exp_code
     assert bad == nblk + single_bad
+
+
+@pytest.mark.parametrize("cap", [8, 64, 4096, 100000])
+def test_device_compress_capacity_is_respected(codec, golden, oracle, cap):
+    """compress_device into a slot smaller than the payload: MYYUV_E_CAPACITY,
+    the true size is still reported, and no byte past `cap` is written
+    (canary after the slot); the tile writers skip what does not fit."""
+    import torch
+    import myyuv_hip
+    raw = golden("chef-with-trumpet.myyuv")
+    w, h, q = raw.width, raw.height, (50, 50, 50)
+    want = oracle.compress(raw.data, w, h, q)
+    assert cap < len(want)
+    dev = torch.device("cuda", 0)
+    d_in = torch.frombuffer(bytearray(raw.data), dtype=torch.uint8).to(dev)
+    d_pay = torch.full((cap + 4096,), 0xA5, dtype=torch.uint8, device=dev)
+    d_size = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    codec.compress_device(d_in.data_ptr(), w, h, q, d_pay.data_ptr(), cap, d_size.data_ptr(), st.cuda_stream)
+    rc, _ = codec.sync_status(st.cuda_stream)
+    assert rc == myyuv_hip.E_CAPACITY
+    assert int(d_size.item()) == len(want)
+    tail = d_pay[cap:].cpu()
+    assert bool((tail == 0xA5).all())

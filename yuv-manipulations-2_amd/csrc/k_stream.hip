@@ -200,7 +200,8 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
       for (int k = 0; k < 8; k++) o[hpos + k] = (uint8_t)(vals[k >> 2] >> (8 * (k & 3)));
     }
     const uint32_t psize = 8 + nb + content;
-    for (int k = 0; k < 4; k++) o[4 * p + k] = (uint8_t)(psize >> (8 * k));
+    for (int k = 0; k < 4; k++)
+      if (4u * p + k < cap) o[4 * p + k] = (uint8_t)(psize >> (8 * k));
     if (p == 0) {
       const uint64_t bytes = 12ull + 24ull + G.cum[3] + total;
       out_size[f] = (uint32_t)bytes;

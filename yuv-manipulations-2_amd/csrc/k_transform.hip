@@ -71,6 +71,9 @@
 #ifndef MYYUV_EXP
 #define MYYUV_EXP 0  // diagnostic ablations (tools/kab.sh builds); 0 = the product
 #endif
+#ifndef MYYUV_K1_PRIO
+#define MYYUV_K1_PRIO 0  // s_setprio level of K1's waves (tuning builds)
+#endif
 #ifdef MYYUV_XF_OCC  // register budget for MYYUV_XF_OCC waves per SIMD (tuning builds)
 #define MYYUV_XF_ATTR __attribute__((amdgpu_waves_per_eu(MYYUV_XF_OCC, MYYUV_XF_OCC)))
 #else
@@ -87,6 +90,10 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
                                                    const QTables* __restrict__ qt,
                                                    uint4* __restrict__ coef, uint8_t* __restrict__ rmask,
                                                    uint4* __restrict__ sink, uint32_t* __restrict__ k2ctl) {
+#if MYYUV_K1_PRIO > 0
+  // wave issue priority over the other launch groups' kernels on the SIMD
+  __builtin_amdgcn_s_setprio(MYYUV_K1_PRIO);
+#endif
   // K2's overflow count for the launch that follows in the stream (nullptr: none)
   if (k2ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *k2ctl = 0u;
   __shared__ float tile[4][kXfUnit * kTile];
