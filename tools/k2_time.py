@@ -40,9 +40,9 @@ def run(raw, w, h, q, label, iters=10):
     fs = np.zeros(8192 * 8, np.uint32)
     L.myyuv_debug_k2_fstamps(fs.ctypes.data_as(ctypes.c_void_p), 8192)
     fs8 = fs.reshape(-1, 8)
-    cls_names = {0: 'single', 1: 'r4', 2: 'r8'}
+    cls_names = {0: 'single', 1: 'r4', 2: 'r8', 3: 'r8x'}
     used = fs8[:, 7] > 0
-    for cl in (0, 1, 2):
+    for cl in (0, 1, 2, 3):
         sel = used & ((fs8[:, 0] & 0xFF) == cl)
         if sel.any():
             st = fs8[sel]
@@ -80,5 +80,4 @@ g = myyuv_file.YUVFile.load(os.path.join(R, 'tests/golden/chef-with-trumpet-big-
 w, h = g.width, g.height
 raw = O.decompress(g.data, w, h, tuple(g.params))
 run(raw, w, h, 50, 'chef-big q50')
-run(raw, w, h, 90, 'chef-big q90')
 run(synth.noise_frame(2048, 1024).tobytes(), 2048, 1024, 50, 'noise q50')
