@@ -201,8 +201,8 @@ struct CoefRegs {
 //     symbols, so the freq[0] probe is invisible): runs of a bucket in
 //     decreasing first insertion, each run in decreasing insertion order;
 //   * the libstdc++ heap (push_heap / pop_heap, __adjust_heap) on 8 registers,
-//     specialised for at most 8 entries: pop's hole descends at most two
-//     levels and every child it compares is one of two candidates;
+//     specialised for at most 8 entries: a pop or push is a merge of one
+//     entry into a root path of at most three entries (pop / push below);
 //   * parents, depths, per-length counts, canonical first codes: packed
 //     nibble / byte fields.
 // Same bytes as encode_block.
@@ -232,71 +232,90 @@ MYYUV_HD void hset(uint32_t (&H)[CAP], uint32_t i, uint32_t x) {
   for (int s = lo; s <= hi; s++) H[s] = i == (uint32_t)s ? x : H[s];
 }
 
-// __push_heap from `hole` (in [0, maxhole]): sift up while parent.freq > e.freq.
-template <int maxhole, int CAP>
-MYYUV_HD void sift_up(uint32_t (&H)[CAP], uint32_t hole, uint32_t e) {
-  bool go = true;
+// Heap entries are freq << 8 | id with freq < 256, so fq(a) <= fq(b) is
+// a <= (b | 0xFF) and fq(a) > fq(b) is a > (b | 0xFF): one compare.
+MYYUV_HD bool fq_gt(uint32_t a, uint32_t b) { return a > (b | 0xFFu); }
+
+// std::priority_queue::pop (libstdc++ __pop_heap + __adjust_heap, then
+// __push_heap of the last element from the hole) for a heap that keeps m
+// entries, m in [0, CAP-1]; returns the old top.  __adjust_heap walks a path
+// down from the root, moving each path entry up one level; __push_heap then
+// sifts the old last element v back up the same path.  The path entries are
+// in heap order, so the result is v merged into the path: the r path
+// entries with freq <= fq(v) stay above it, the others move down one.  With
+// at most 7 entries left the path is the root, one child c1 (when m >= 2)
+// and one grandchild c2 (m >= 4; CAP 8): the whole pop is two compares for
+// the path, one for r per level and a select per touched position.
+template <int CAP>
+MYYUV_HD uint32_t pop(uint32_t (&H)[CAP], uint32_t m) {
+  // (the entries are copied to scalars: a select between two elements of
+  // the array would be folded into a dynamically indexed load, which moves
+  // the array out of registers)
+  uint32_t x[8];
 #pragma unroll
-  for (int lvl = 0; lvl < 3; lvl++) {
-    if ((maxhole >> lvl) == 0) break;  // hole < 2^(lvl): nothing above
-    const uint32_t par = (hole - 1) >> 1;
-    const uint32_t pe = hget<CAP>(H, par);
-    const bool mv = go && hole > 0 && fq(pe) > fq(e);
-    // hole's possible values at this level: [1, maxhole >> lvl] roughly; the
-    // select network covers [1, 7] and folds for static holes
-    if (mv) hset<1, CAP - 1>(H, hole, pe);
-    hole = mv ? par : hole;
-    go = mv;
+  for (int k = 0; k < 8; k++) x[k] = k < CAP ? H[k < CAP ? k : 0] : 0u;
+  const uint32_t top = x[0];
+  const uint32_t v = hget<CAP>(H, m);
+  const uint32_t vh = v | 0xFFu;
+  // level 1: child 2 unless freq[2] > freq[1] (m >= 3); child 1 when m = 2
+  const bool l1 = m >= 2;
+  const bool c1is1 = !(m >= 3) || fq_gt(x[2], x[1]);
+  const uint32_t a0 = c1is1 ? x[1] : x[2];
+  const bool r1 = l1 && a0 <= vh;
+  const uint32_t new0 = r1 ? a0 : v;
+  uint32_t new1 = r1 ? v : a0;  // (used when l1)
+  if constexpr (CAP == 8) {
+    // level 2: the loop goes on while c1 < (m - 1) / 2; an even m ends on the
+    // last internal node's single (left) child: (m, c1) = (4, 1) or (6, 2)
+    const bool loop2 = c1is1 ? m >= 5 : m >= 7;
+    const bool spec2 = c1is1 ? m == 4 : m == 6;
+    const bool l2 = loop2 || spec2;
+    const uint32_t lt = c1is1 ? x[3] : x[5], rt = c1is1 ? x[4] : x[6];
+    const bool left = spec2 || fq_gt(rt, lt);
+    const uint32_t a1 = left ? lt : rt;
+    const bool r2 = l2 && r1 && a1 <= vh;
+    new1 = r2 ? a1 : new1;
+    const uint32_t new2 = r2 ? v : a1;
+    H[3] = (l2 && c1is1 && left) ? new2 : x[3];
+    H[4] = (l2 && c1is1 && !left) ? new2 : x[4];
+    H[5] = (l2 && !c1is1 && left) ? new2 : x[5];
+    H[6] = (l2 && !c1is1 && !left) ? new2 : x[6];
   }
-  hset<0, CAP - 1>(H, hole, e);
+  H[0] = new0;
+  H[1] = (l1 && c1is1) ? new1 : x[1];
+  H[2] = (l1 && !c1is1) ? new1 : x[2];
+  return top;
 }
 
-// std::priority_queue::pop (libstdc++ __pop_heap + __adjust_heap) for a heap
-// of len in [1, CAP] entries; returns the old top.
+// std::priority_queue::push (__push_heap) of e at the hole h = current size,
+// h in [0, CAP-1]: the ancestors of h with freq > fq(e) (a bottom part of
+// the ancestor chain) move down one level, e takes the freed position.
 template <int CAP>
-MYYUV_HD uint32_t pop(uint32_t (&H)[CAP], uint32_t& len) {
-  const uint32_t top = H[0];
-  const uint32_t m = --len;  // entries left
-  if (m > 0) {
-    const uint32_t value = hget<CAP>(H, m);
-    // __adjust_heap(first, 0, m, value): second child walk
-    uint32_t hole = 0, sc = 0;
-    const bool it1 = m >= 3;  // 0 < (m - 1) / 2
-    const uint32_t c1 = fq(H[2]) > fq(H[1]) ? 1u : 2u;
-    if (it1) {
-      H[0] = c1 == 1 ? H[1] : H[2];
-      hole = c1;
-      sc = c1;
-    }
-    if constexpr (CAP == 8) {
-      const bool it2 = it1 && (c1 == 1 ? m >= 5 : m >= 7);  // sc < (m - 1) / 2
-      const uint32_t rt = c1 == 1 ? H[4] : H[6], lt = c1 == 1 ? H[3] : H[5];
-      const bool left = fq(rt) > fq(lt);
-      const uint32_t c2 = 2 * c1 + 2 - (left ? 1u : 0u);
-      if (it2) {
-        const uint32_t pv = left ? lt : rt;
-        H[1] = c1 == 1 ? pv : H[1];
-        H[2] = c1 == 2 ? pv : H[2];
-        hole = c2;
-        sc = c2;
-      }
-    }
-    // even length, last internal node with a single child
-    if ((m & 1) == 0 && sc == (m - 2) / 2) {
-      const uint32_t ch = 2 * sc + 1;  // (m, sc) in {(2,0), (4,1), (6,2)}
-      if constexpr (CAP == 4) {
-        H[0] = H[1];  // m = 2
-      } else {
-        const uint32_t cv = sc == 0 ? H[1] : (sc == 1 ? H[3] : H[5]);
-        H[0] = sc == 0 ? cv : H[0];
-        H[1] = sc == 1 ? cv : H[1];
-        H[2] = sc == 2 ? cv : H[2];
-      }
-      hole = ch;
-    }
-    sift_up<CAP - 2, CAP>(H, hole, value);
+MYYUV_HD void push(uint32_t (&H)[CAP], uint32_t h, uint32_t e) {
+  uint32_t x[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = k < CAP ? H[k < CAP ? k : 0] : 0u;
+  const uint32_t eh = e | 0xFFu;
+  const uint32_t p1 = (h - 1) >> 1;   // parent, [0, 3] (h >= 1)
+  const uint32_t p2 = (p1 - 1) >> 1;  // grandparent, [0, 1] (h >= 3)
+  const uint32_t b1 = (p1 & 2) ? ((p1 & 1) ? x[3] : x[2]) : ((p1 & 1) ? x[1] : x[0]);
+  const uint32_t b2 = p2 == 0 ? x[0] : x[1];
+  const bool m1 = h >= 1 && b1 > eh;
+  const bool m2 = m1 && h >= 3 && b2 > eh;
+  const bool m3 = CAP > 4 && m2 && h >= 7 && x[0] > eh;  // h = 7: p1 = 3, p2 = 1, then the root
+  const uint32_t nh = m1 ? b1 : e;
+  const uint32_t np1 = m2 ? b2 : (m1 ? e : b1);
+  const uint32_t np2 = m3 ? x[0] : (m2 ? e : b2);
+  // positions written are distinct: root < p2 < p1 < h
+#pragma unroll
+  for (int k = 0; k < CAP; k++) {
+    uint32_t y = x[k];
+    if (k <= 1) y = (h >= 3 && p2 == (uint32_t)k) ? np2 : y;
+    if (k <= 3) y = (h >= 1 && p1 == (uint32_t)k) ? np1 : y;
+    y = h == (uint32_t)k ? nh : y;
+    if (k == 0 && CAP > 4) y = m3 ? e : y;
+    H[k] = y;
   }
-  return top;
 }
 
 // field i (dynamic, [0, CAP)) of CAP x 16-bit fields in CAP / 2 dwords
@@ -418,22 +437,21 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
   R8_STAMP(2);
   // ---------------- 3. Huffman merges on the libstdc++ heap ----------------
   uint32_t H[CAP] = {};
-  uint32_t hlen = 0;
 #pragma unroll
   for (int r = 0; r < CAP; r++) {
     if ((uint32_t)r < n) {
       const uint32_t k = (ord >> (4 * r)) & 15u;
       const uint32_t e = (((uint32_t)(cnt >> (8 * k)) & 0xFFu) << 8) | k;
-      sift_up<CAP - 1, CAP>(H, (uint32_t)r, e);
-      hlen++;
+      push<CAP>(H, (uint32_t)r, e);
     }
   }
   uint32_t lpar = 0, ipar = 0;  // parent (merge index) of leaf k / internal j, nibbles
 #pragma unroll
   for (int j = 0; j < CAP - 1; j++) {
     if ((uint32_t)j + 1 < n) {
-      const uint32_t l = pop<CAP>(H, hlen);
-      const uint32_t r = pop<CAP>(H, hlen);
+      // the heap holds n - j entries
+      const uint32_t l = pop<CAP>(H, n - 1 - (uint32_t)j);
+      const uint32_t r = pop<CAP>(H, n - 2 - (uint32_t)j);
 #pragma unroll
       for (int s = 0; s < 2; s++) {
         const uint32_t id = (s == 0 ? l : r) & 0xFFu;
@@ -442,8 +460,7 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
         if (id < 8) lpar = (lpar & m) | v;
         else ipar = (ipar & m) | v;
       }
-      sift_up<CAP - 2, CAP>(H, hlen, ((fq(l) + fq(r)) << 8) | (8u + (uint32_t)j));
-      hlen++;
+      push<CAP>(H, n - 2 - (uint32_t)j, ((fq(l) + fq(r)) << 8) | (8u + (uint32_t)j));
     }
   }
   // depths of internal nodes (root = n - 2 at depth 0), then code lengths
