@@ -13,7 +13,7 @@ import torch  # noqa: E402
 import myyuv_file  # noqa: E402
 import myyuv_hip  # noqa: E402
 
-NF, B, GROUPS = 3, 4, 45
+NF, B, GROUPS = 3, 6, 30
 g = myyuv_file.YUVFile.load(os.path.join(ROOT, "tests/golden/chef-with-trumpet-big-DCT-50.myyuv"))
 w, h = g.width, g.height
 L = myyuv_hip.load()

@@ -208,6 +208,10 @@ struct CoefRegs {
 // Same bytes as encode_block.
 // ---------------------------------------------------------------------------
 
+// Positions per wave-uniform step of the per-position loops (the loops run to
+// the wave's longest message).
+constexpr int kPosGroup = 4;
+
 namespace rr {
 
 MYYUV_HD uint32_t fq(uint32_t e) { return e >> 8; }
@@ -364,10 +368,10 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
   SlotIds<CAP> ids;
   ids.clear();
 #pragma unroll
-  for (int i0 = 0; i0 < 64; i0 += 8) {
+  for (int i0 = 0; i0 < 64; i0 += kPosGroup) {
     if (i0 < wave_msz) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
+      for (int k = 0; k < kPosGroup; k++) {
         const int i = i0 + k;
         const int v = R.sym(i);
         const bool act = i < msz && !ovf;
@@ -390,7 +394,7 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
         if (act) cnt += 1ull << (8 * (sl & 7));
         n += ins ? 1u : 0u;
         has_zero = has_zero || (act && v == 0);
-        ids.set(i, act ? (sl & 7) : 0u);
+        ids.set(i, sl);  // (read for i < msz only: sl <= 7 there unless the block overflows)
       }
     }
   }
@@ -573,17 +577,19 @@ MYYUV_HD void emit_chunk(const EncState& S, int wave_msz, W& bw) {
     }
   }
   bw.align_byte();
+  // the code bits, four positions (<= 32 bits) per put
 #pragma unroll
-  for (int i0 = 0; i0 < 64; i0 += 8) {
+  for (int i0 = 0; i0 < 64; i0 += 4) {
     if (i0 < wave_msz) {
+      uint32_t bits = 0, nb = 0;
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
+      for (int k = 0; k < 4; k++) {
         const int i = i0 + k;
-        if ((uint32_t)i < S.msz) {
-          const uint32_t ct = rr::f16<8>(S.CT, S.ids.get(i));
-          bw.put(ct & 0xFFu, (int)(ct >> 8));
-        }
+        const uint32_t ct = (uint32_t)i < S.msz ? rr::f16<8>(S.CT, S.ids.get(i)) : 0u;
+        bits |= (ct & 0xFFu) << nb;
+        nb += ct >> 8;
       }
+      bw.put(bits, (int)nb);
     }
   }
 }
