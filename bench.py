@@ -456,6 +456,15 @@ def main():
                        "unit": "GB/s", "frac": round(a6 / HBM_PEAK_GBS, 4),
                        "algorithmic_bytes_per_launch": 3 * samples * B,
                        "avg_launch_us": kernel_us["dequant_idct"]}
+        # the fused decoder (default; K5 + K6 in one kernel, the "huff_decode"
+        # id): stream bytes in + 1 B per sample out
+        roof_dec = None
+        if not kernel_us.get("dequant_idct") and kernel_us.get("huff_decode"):
+            alg_d = (n0 + samples) * B
+            ad = alg_d / (kernel_us["huff_decode"] * 1e-6) / 1e9
+            roof_dec = {"kernel": "decode_idct (fused K5+K6)", "achieved": round(ad, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ad / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": alg_d,
+                        "avg_launch_us": kernel_us["huff_decode"]}
         for k, us in kernel_us.items():
             log(f"kernel {k:16s} {us:9.2f} us/launch")
         cpu = None
@@ -474,6 +483,7 @@ def main():
                        "frames_per_step": per_step, "launch_groups_in_flight": nf,
                        "frames_per_launch": B, "input_copies": nin, "payload_bytes": n0},
             "roofline": roof, "roofline_isolated": roof_iso, "roofline_idct_isolated": roof_k6,
+            "roofline_decode_isolated": roof_dec,
             "cpu_baseline": cpu,
             "kernel_us": kernel_us or None,
             "side": side,

@@ -35,20 +35,25 @@ def oracle():
 
 @pytest.fixture(scope="session", params=["split", "fused"])
 def codec(request):
-    """A codec context per encoder: K1 -> K2 through HBM ("split") and the
-    fused single-pass encoder k_encode_tile ("fused"; MYYUV_ENCODER is read
-    when the context is created).  Every test taking `codec` runs on both."""
+    """A codec context per kernel arrangement: "split" (K1 -> K2 and K5 -> K6
+    through HBM) and "fused" (the single-pass encoder k_encode_tile and the
+    single-pass decoder k_decode_idct, the decoder's default; MYYUV_ENCODER /
+    MYYUV_DECODER are read when the context is created).  Every test taking
+    `codec` runs on both."""
     import myyuv_hip
 
-    old = os.environ.get("MYYUV_ENCODER")
-    os.environ["MYYUV_ENCODER"] = request.param
+    keys = ("MYYUV_ENCODER", "MYYUV_DECODER")
+    old = {k: os.environ.get(k) for k in keys}
+    for k in keys:
+        os.environ[k] = request.param
     try:
         c = myyuv_hip.Codec(0)
     finally:
-        if old is None:
-            del os.environ["MYYUV_ENCODER"]
-        else:
-            os.environ["MYYUV_ENCODER"] = old
+        for k in keys:
+            if old[k] is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = old[k]
     yield c
     c.close()
 

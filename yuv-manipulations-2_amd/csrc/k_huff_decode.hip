@@ -35,6 +35,7 @@
 //   written as 8 quads of the codec_common.hpp layout that K6 reads.
 #include "codec_common.hpp"
 #include "k_stream.hpp"
+#include "xform_common.hpp"
 
 namespace myyuv_gpu {
 
@@ -275,18 +276,22 @@ __device__ __forceinline__ int decode_general(const LdsChunk c, const Table T, u
 
 }  // namespace
 
-__global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_t* __restrict__ in,
-                                                   const uint32_t* __restrict__ in_size,
-                                                   uint32_t cap,
-                                                   const StreamDesc* __restrict__ desc,
-                                                   const uint32_t* __restrict__ local_off,
-                                                   const uint32_t* __restrict__ tile_pre,
-                                                   FrameGeom G, uint32_t tiles_p0,
-                                                   uint32_t tiles_p1,
-                                                   uint4* __restrict__ coef,
-                                                   uint8_t* __restrict__ rmask,
-                                                   unsigned long long* __restrict__ err) {
-  __shared__ uint4 stq[kStageQuads];
+// K5's decode of one wave's 64-block group (blockIdx.x) of frame blockIdx.y:
+// the natural-order words of each lane's block in nw (or, for a table that is
+// not "regular", written to coef by decode_general: *direct).  Returns false
+// when the frame's stream header is bad (nothing decoded).
+struct DecodeGroup {
+  uint32_t f, gbase, g0, g1, g;
+  int p;
+  bool live;
+};
+__device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, const uint32_t* __restrict__ in_size,
+                                             uint32_t cap, const StreamDesc* __restrict__ desc,
+                                             const uint32_t* __restrict__ local_off,
+                                             const uint32_t* __restrict__ tile_pre, const FrameGeom& G,
+                                             uint32_t tiles_p0, uint32_t tiles_p1, uint4* __restrict__ coef,
+                                             unsigned long long* __restrict__ err, uint4* stq, DecodeGroup& D,
+                                             uint32_t (&nw)[32], bool& direct) {
   // frame blockIdx.y of the batch: its stream slot, descriptor and scan;
   // coefficients at batch-global block gbase + g
   const uint32_t f = blockIdx.y;
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
   desc += f;
   local_off += gbase;
   tile_pre += (size_t)f * (ntiles + 1);
-  if (desc->bad) return;
+  if (desc->bad) return false;
   const int lane = threadIdx.x;
   const uint32_t t = blockIdx.x;
   const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
@@ -327,11 +332,8 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
     ok = false;
   }
 
-  uint32_t nw[32];
-#pragma unroll
-  for (int w = 0; w < 32; w++) nw[w] = 0;
   int code = 0;
-  bool direct = false;  // block written by decode_general
+  direct = false;  // block written by decode_general
 
   // Rounds: stage the chunks of the first pending lane onwards (as many as
   // the stage holds, bytes at or past `limit` read as 0, one zero quad after),
@@ -403,7 +405,41 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
     __syncthreads();  // the next round overwrites the stage
   }
   if (ok && code) record_error(err, 2ull * (gbase + g) + 1, code);
+  D.f = f;
+  D.gbase = gbase;
+  D.g0 = g0;
+  D.g1 = g1;
+  D.g = g;
+  D.p = p;
+  D.live = live;
+  return true;
+}
 
+__global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_t* __restrict__ in,
+                                                   const uint32_t* __restrict__ in_size,
+                                                   uint32_t cap,
+                                                   const StreamDesc* __restrict__ desc,
+                                                   const uint32_t* __restrict__ local_off,
+                                                   const uint32_t* __restrict__ tile_pre,
+                                                   FrameGeom G, uint32_t tiles_p0,
+                                                   uint32_t tiles_p1,
+                                                   uint4* __restrict__ coef,
+                                                   uint8_t* __restrict__ rmask,
+                                                   unsigned long long* __restrict__ err) {
+  __shared__ uint4 stq[kStageQuads];
+  if (desc[blockIdx.y].bad) return;
+  DecodeGroup D;
+  uint32_t nw[32];
+#pragma unroll
+  for (int w = 0; w < 32; w++) nw[w] = 0;
+  bool direct;
+  decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw, direct);
+  const uint32_t gbase = blockIdx.y * G.cum[3];
+  const uint32_t t = blockIdx.x;
+  const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
+  const uint32_t tile_in_plane = t - (p == 0 ? 0 : (p == 1 ? tiles_p0 : tiles_p0 + tiles_p1));
+  const uint32_t g = G.cum[p] + tile_in_plane * kWave + threadIdx.x;
+  const bool live = g < min(G.cum[p] + tile_in_plane * kWave + kWave, G.cum[p + 1]);
   // ---- natural-order words to the quad layout (1 KiB contiguous per store)
   // Only the nonzero rows are stored; bit c of the block's row mask says
   // whether row c holds a nonzero coefficient, and K6 reads just those.
@@ -420,6 +456,84 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_
       }
     }
     rmask[gbase + g] = (uint8_t)m;
+  }
+}
+
+// Fused decoder (K5 + K6; MYYUV_DECODER=fused): the wave decodes its 64-block
+// group as K5 does, then runs K6's transform on it as four 16-block units
+// straight from its registers: the unit's 16 decoding lanes write their
+// blocks' int16 images into the wave's transpose tile (laid over the chunk
+// stage, dead by then), and the wave's lanes take K6's (block, quarter)
+// roles (idct_rows, xform_common.hpp).  The coefficients never reach HBM.
+__global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_t* __restrict__ in,
+                                                   const uint32_t* __restrict__ in_size,
+                                                   uint32_t cap,
+                                                   const StreamDesc* __restrict__ desc,
+                                                   const uint32_t* __restrict__ local_off,
+                                                   const uint32_t* __restrict__ tile_pre,
+                                                   FrameGeom G, uint32_t tiles_p0,
+                                                   uint32_t tiles_p1, const QTables* __restrict__ qt,
+                                                   uint4* __restrict__ coef,
+                                                   uint8_t* __restrict__ frame,
+                                                   unsigned long long* __restrict__ err) {
+  static_assert(sizeof(uint4) * kStageQuads >= sizeof(float) * xf::kXfTile16, "the tile over the stage");
+  __shared__ uint4 stq[kStageQuads];
+  __shared__ float sq[64];
+  const uint32_t lane = threadIdx.x;
+  {
+    const uint32_t t = blockIdx.x;
+    const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
+    sq[lane] = qt->q[p][lane];  // (ordered before idct_rows by decode_group's barriers)
+  }
+  if (desc[blockIdx.y].bad) return;
+  DecodeGroup D;
+  uint32_t nw[32];
+#pragma unroll
+  for (int w = 0; w < 32; w++) nw[w] = 0;
+  bool direct;
+  decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw, direct);
+  if (D.live && direct) {  // decode_general wrote the block to coef (a table the reference never writes)
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint4 v = coef[coef_quad(D.gbase + D.g, c)];
+      nw[4 * c] = v.x;
+      nw[4 * c + 1] = v.y;
+      nw[4 * c + 2] = v.z;
+      nw[4 * c + 3] = v.w;
+    }
+  }
+  // ---- K6 on the group, unit by unit
+  const int p = D.p;
+  xf::Unit U;
+  U.p = p;
+  U.cum = G.cum[p];
+  U.nb = G.cum[p + 1] - G.cum[p];
+  U.poff = p == 0 ? G.poff[0] : (p == 1 ? G.poff[1] : G.poff[2]);
+  U.pw = p == 0 ? G.pw[0] : (p == 1 ? G.pw[1] : G.pw[2]);
+  U.bw = p == 0 ? G.bw[0] : (p == 1 ? G.bw[1] : G.bw[2]);
+  U.bmag = p == 0 ? G.bmag[0] : (p == 1 ? G.bmag[1] : G.bmag[2]);
+  U.local0 = 0;
+  float* tile = reinterpret_cast<float*>(stq);
+  const uint32_t q = lane & 3u, b = lane >> 2;
+  uint8_t* fr = frame + (size_t)D.f * G.fbytes;
+#pragma unroll 1
+  for (uint32_t u = 0; u < 4; u++) {
+    const uint32_t ub = D.g0 + 16u * u;  // the unit's first block
+    if (ub >= D.g1) break;
+    if ((lane >> 4) == u) {
+      uint4* img = reinterpret_cast<uint4*>(tile + (lane & 15u) * xf::kTile);
+#pragma unroll
+      for (int c = 0; c < 8; c++) img[c] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
+    }
+    xf::wave_sync();
+    uint2 w0, w1;
+    xf::idct_rows(tile + b * xf::kTile, q, sq, w0, w1);
+    if (ub + b < D.g1) {
+      const uint32_t off = xf::block_row_offset(U, ub + b - U.cum, 2u * q);
+      *reinterpret_cast<uint2*>(fr + off) = w0;
+      *reinterpret_cast<uint2*>(fr + off + U.pw) = w1;
+    }
+    xf::wave_sync();  // the next unit rewrites the tile
   }
 }
 

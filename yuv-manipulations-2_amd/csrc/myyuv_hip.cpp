@@ -26,6 +26,9 @@ namespace myyuv_gpu {
 __global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*);
 __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*,
                                uint4*);
+__global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*, const uint32_t*,
+                              const uint32_t*, FrameGeom, uint32_t, uint32_t, const QTables*, uint4*, uint8_t*,
+                              unsigned long long*);
 __global__ void k_huff_encode(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
                               uint8_t*, uint16_t*, uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
@@ -180,6 +183,9 @@ struct myyuv_hip_ctx {
   // encoder: K1 -> K2 through HBM (split), or the fused single-pass kernel
   // k_encode_tile (MYYUV_ENCODER=fused|split)
   bool fused = false;
+  // decoder: the fused k_decode_idct (default), or K5 -> K6 through HBM
+  // (MYYUV_DECODER=split)
+  bool fused_dec = true;
   // chained scan (k_chain.hpp): per-tile status words tagged with the launch
   // epoch, counted here
   DevBuf status;
@@ -433,6 +439,12 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
   const uint32_t t0 = ceil_div(G.cum[1] - G.cum[0], kWave),
                  t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
+  if (c->fused_dec) {  // K5 + K6 in one pass, the coefficients kept on chip
+    e |= launch(c, MYYUV_K_HUFF_DEC, k_decode_idct, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size, cap,
+                (const StreamDesc*)desc, c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
+                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err);
+    return e ? MYYUV_E_HIP : 0;
+  }
   e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size,
               cap, (const StreamDesc*)desc, c->loff.as<const uint32_t>(),
               c->tiles.as<const uint32_t>(), G, t0, t1, c->coef.as<uint4>(), c->rmask.as<uint8_t>(), err);
@@ -552,6 +564,8 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
       {
         const char* v = std::getenv("MYYUV_ENCODER");
         c->fused = v && std::strcmp(v, "fused") == 0;
+        const char* d = std::getenv("MYYUV_DECODER");
+        c->fused_dec = !(d && std::strcmp(d, "split") == 0);
       }
       // tuning knobs (diagnostic; default 100): K1 / K6 grids as a percentage
       // of the resident workgroups, leaving wave slots to other launch groups

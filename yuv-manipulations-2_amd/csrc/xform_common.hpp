@@ -12,6 +12,7 @@ namespace xf {
 
 constexpr float c_dct[64] = MYYUV_DCT_MATRIX;  // row u = basis u (DCT.cpp:221-230)
 constexpr int kTile = 72;  // floats per block in the transpose tile; (i, j) at tix(i, j)
+constexpr int kXfTile16 = 16 * kTile;  // a 16-block unit's tile (floats)
 constexpr float kMagic = 0x1.8p23f;             // 1.5 * 2^23
 constexpr float kMagicPx = 0x1.8p23f + 128.0f;  // ... + 128: low byte = pixel
 constexpr float kHalfDown = 0x1.fffffep-2f;     // largest float below 0.5
@@ -258,6 +259,91 @@ __device__ __forceinline__ void pack_quads(const uint32_t (&c)[16], uint32_t q, 
   rm = (nzl ? 1u << (2 * q) : 0u) | (nzh ? 2u << (2 * q) : 0u);
   rm |= __shfl_xor(rm, 1, 64);
   rm |= __shfl_xor(rm, 2, 64);
+}
+
+// K6's body for lane (b, q) of a 16-block unit (DCT.cpp:325-335, :358-362):
+// the block's int16 coefficient image (natural order, word w = coefficients
+// 2w, 2w+1) is the first 32 dwords of its transpose tile tb; Qt: the plane's
+// Q table (natural order).  Out: pixel rows 2q (w0) and 2q+1 (w1), 8 bytes
+// each.  Shared by k_dequant_idct and the fused decoder (k_decode_idct).
+__device__ __forceinline__ void idct_rows(float* tb, uint32_t q, const float* Qt, uint2& w0, uint2& w1) {
+  const uint32_t* tw = reinterpret_cast<const uint32_t*>(tb);
+  // (Z[k][2q], Z[k][2q+1]) = word k*4 + q
+  uint32_t zc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) zc[k] = tw[k * 4 + q];
+  wave_sync();
+  // the quantisers of columns 2q, 2q+1: qk[2k + h] = Q[k][2q + h]
+  float qk[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float2 v = *reinterpret_cast<const float2*>(Qt + k * 8 + 2 * q);
+    qk[2 * k] = v.x;
+    qk[2 * k + 1] = v.y;
+  }
+
+  // ---- dequantise (DCT.cpp:331) and stage 1: U[i][j] = sum_k D[k][i] * Z[k][j],
+  // j in {2q, 2q+1} (squareMatrixMulT2<8>(DCT, Z), DCT.cpp:256-266)
+  // Quantised blocks are sparse: a coefficient row k that is zero in all 16
+  // blocks of the unit (61 % of the (unit, k) pairs of the bench frame)
+  // contributes only +-0 products, and a sum that starts at +0 (as the
+  // reference's does, DCT.cpp:259-263) is unchanged by them — so the wave
+  // skips that step outright, bit-exactly.  Stage 2 skips the zero columns
+  // of Z the same way (U's column k is zero exactly when Z's is).
+  float Um[16];  // Um[2i + h] = U[i][2q + h]
+#pragma unroll
+  for (int j = 0; j < 16; j++) Um[j] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (!__any(zc[k] != 0u)) continue;
+    const float z0 = (float)(int16_t)zc[k] * qk[2 * k];
+    const float z1 = (float)(int16_t)(zc[k] >> 16) * qk[2 * k + 1];
+    float pr[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      pr[2 * i] = c_dct[k * 8 + i] * z0;
+      pr[2 * i + 1] = c_dct[k * 8 + i] * z1;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) Um[j] = Um[j] + pr[j];
+    fence16(Um);
+  }
+
+  // ---- transpose (the float tile reuses the block's LDS)
+  float P[16];  // P[2k + h] = U[2q + h][k]
+  transpose_tile(tb, q, Um, P);
+
+  // ---- stage 2: R[i][v] = sum_k U[i][k] * D[k][v] (squareMatrixMul<8>(U, DCT)),
+  // then clamp(roundf(R) + 128) (DCT.cpp:358-362)
+  float S[16];  // S[2v + h] = R[2q + h][v]
+  dot_rows<true, true>(P, S);
+  uint32_t px[16];  // low byte = pixel
+  bool tie = false;  // an exact .5 in the lane: fract(s') == 0.5 (exact for |s'| <= 128)
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    S[j] = __builtin_amdgcn_fmed3f(S[j], -128.0f, 127.0f);
+    const float uu = S[j] + kMagicPx;
+    tie = tie || __builtin_amdgcn_fractf(S[j]) == 0.5f;
+    px[j] = bits(uu);
+  }
+  if (tie) {  // an exact .5 somewhere in the lane: roundf goes away from zero
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      px[j] = (uint32_t)((int)__builtin_truncf(S[j] + __builtin_copysignf(kHalfDown, S[j])) + 128);
+  }
+  // rows 2q (even j) and 2q+1 (odd j): bytes v = 0..7 of each
+  w0 = make_uint2(__builtin_amdgcn_perm(__builtin_amdgcn_perm(px[6], px[4], 0x0c0c0400u),
+                                                    __builtin_amdgcn_perm(px[2], px[0], 0x0c0c0400u),
+                                                    0x05040100u),
+                              __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[14], px[12], 0x0c0c0400u),
+                                                    __builtin_amdgcn_perm(px[10], px[8], 0x0c0c0400u),
+                                                    0x05040100u));
+  w1 = make_uint2(__builtin_amdgcn_perm(__builtin_amdgcn_perm(px[7], px[5], 0x0c0c0400u),
+                                                    __builtin_amdgcn_perm(px[3], px[1], 0x0c0c0400u),
+                                                    0x05040100u),
+                              __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[15], px[13], 0x0c0c0400u),
+                                                    __builtin_amdgcn_perm(px[11], px[9], 0x0c0c0400u),
+                                                    0x05040100u));
 }
 
 }  // namespace xf
