@@ -32,6 +32,18 @@ MYYUV_HD uint32_t hd_brev(uint32_t x) {
 #endif
 }
 MYYUV_HD uint32_t hd_clz(uint32_t x) { return (uint32_t)__builtin_clz(x); }  // x != 0
+MYYUV_HD uint32_t hd_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x); }  // x != 0
+// v_perm_b32: byte i of the result = byte sel.byte[i] (0..7) of {hi, lo}
+MYYUV_HD uint32_t hd_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+  const uint64_t v = ((uint64_t)hi << 32) | lo;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; i++) r |= (uint32_t)((v >> (8 * ((sel >> (8 * i)) & 7u))) & 0xFFu) << (8 * i);
+  return r;
+#endif
+}
 
 // Bucket-count phases of the prime rehash policy for <= 65 elements
 // (_Prime_rehash_policy::_M_next_bkt / _M_need_rehash): 13 buckets from the
@@ -353,6 +365,22 @@ struct EncState {
   SlotIds<8> ids;    // per position: slot of its symbol
 };
 
+// The slot of the tagged key pair vv (the key in both 16-bit fields) among
+// the NP key pairs KP (field k = slot k; empty fields are 0): SWAR zero-field
+// tests, the match bits gathered one per byte (slot k < 4 at bit 8k + 7,
+// slot k >= 4 at bit 8(k - 4) + 3) and located with one bit scan.
+template <int NP>
+MYYUV_HD bool match_slot(const uint32_t (&KP)[NP], uint32_t vv, uint32_t& slot) {
+  uint32_t mp[NP];
+#pragma unroll
+  for (int p = 0; p < NP; p++) mp[p] = ~(((KP[p] ^ vv) | 0x80008000u) - 0x00010001u) & 0x80008000u;
+  uint32_t oh = hd_perm(mp[1 % NP], mp[0], 0x07050301u);
+  if constexpr (NP == 4) oh |= hd_perm(mp[3 % NP], mp[2 % NP], 0x07050301u) >> 4;
+  const uint32_t t = hd_ctz(oh | 0x80000000u);
+  slot = (t >> 3) | ((t & 4u) ^ 4u);
+  return oh != 0;
+}
+
 template <int CAP>
 MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
   using namespace rr;
@@ -363,8 +391,7 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
   // ---------------- 1. distinct symbols, counts, per-position slots ----------------
   uint32_t KP[NP] = {};  // tagged keys, field k = slot k
   uint64_t cnt = 0;               // count of slot k in byte k
-  uint32_t n = 0;
-  bool has_zero = false, ovf = false;
+  uint32_t n = 0;                 // distinct symbols seen (past CAP: the block overflows)
   SlotIds<CAP> ids;
   ids.clear();
 #pragma unroll
@@ -374,37 +401,39 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
       for (int k = 0; k < kPosGroup; k++) {
         const int i = i0 + k;
         const int v = R.sym(i);
-        const bool act = i < msz && !ovf;
+        const bool act = i < msz;
         const uint32_t f = 0x800u | ((uint32_t)v & 0x7FFu);
         const uint32_t vv = f | (f << 16);
-        uint32_t oh = 0;  // one-hot over slots: pair p's fields at bits 15 - p / 31 - p
-#pragma unroll
-        for (int p = 0; p < NP; p++)
-          oh |= (~(((KP[p] ^ vv) | 0x80008000u) - 0x00010001u) & 0x80008000u) >> p;
-        const bool found = oh != 0;
-        const uint32_t b = 31u - hd_clz(oh | 1u);  // the one set bit: 12..15 or 28..31 when found
-        const uint32_t idx = b >= 28 ? 2 * (31 - b) + 1 : 2 * (15 - b);
+        uint32_t sl;
+        const bool found = match_slot<NP>(KP, vv, sl);
         const bool add = act && !found;
-        ovf = ovf || (add && n == CAP);
         const bool ins = add && n < CAP;
-        const uint32_t sl = found ? idx : n;
+        sl = found ? sl : n;
         const uint32_t ishift = (n & 1) * 16;
 #pragma unroll
         for (int p = 0; p < NP; p++) KP[p] |= (ins && (n >> 1) == (uint32_t)p) ? f << ishift : 0u;
-        if (act) cnt += 1ull << (8 * (sl & 7));
-        n += ins ? 1u : 0u;
-        has_zero = has_zero || (act && v == 0);
+        // every processed position is counted; the zeros past the message are
+        // taken off below
+        cnt += 1ull << (8 * (sl & 7));
+        n += add ? 1u : 0u;
         ids.set(i, sl);  // (read for i < msz only: sl <= 7 there unless the block overflows)
       }
     }
   }
-  if (ovf) return false;
+  if (n > (uint32_t)CAP) return false;
   if (msz == 0) {  // all-zero block: one symbol 0, count 1 (Huffman.cpp:191-194)
     KP[0] = 0x800u;
     cnt = 1;
     n = 1;
     msz = 1;
-    has_zero = true;
+  } else {
+    // positions msz .. P - 1 (P: the positions the loop ran, a multiple of
+    // kPosGroup) are zeros: counted into the zero's slot, or into slot n & 7
+    // when the message has no zero (slot n is unused; n = 8 wraps to slot 0)
+    const uint32_t P = (uint32_t)min((wave_msz + kPosGroup - 1) / kPosGroup * kPosGroup, 64);
+    uint32_t zs;
+    const bool zf = match_slot<NP>(KP, 0x08000800u, zs);
+    cnt -= (uint64_t)(P - (uint32_t)msz) << (8 * ((zf ? zs : n) & 7u));
   }
 
   R8_STAMP(1);
