@@ -361,7 +361,8 @@ struct EncState {
   uint32_t msz;      // message length (positions)
   uint64_t lcount;   // per code length L: symbols of that length (byte L - 1)
   uint32_t TK[4];    // table in canonical order: entry r = key & 0x7FF | len << 11 (16-bit fields)
-  uint32_t CT[4];    // per slot k: len << 8 | bit-reversed code (16-bit fields)
+  uint64_t cc;       // per slot k: its bit-reversed code in byte k
+  uint32_t ll;       // per slot k: its code length in nibble k
   SlotIds<8> ids;    // per position: slot of its symbol
 };
 
@@ -371,11 +372,13 @@ struct EncState {
 // slot k >= 4 at bit 8(k - 4) + 3) and located with one bit scan.
 template <int NP>
 MYYUV_HD bool match_slot(const uint32_t (&KP)[NP], uint32_t vv, uint32_t& slot) {
+  // per pair, bits 15 / 31 flag fields 0 / 1 (the other bits are junk and
+  // masked off after the gather)
   uint32_t mp[NP];
 #pragma unroll
-  for (int p = 0; p < NP; p++) mp[p] = ~(((KP[p] ^ vv) | 0x80008000u) - 0x00010001u) & 0x80008000u;
-  uint32_t oh = hd_perm(mp[1 % NP], mp[0], 0x07050301u);
-  if constexpr (NP == 4) oh |= hd_perm(mp[3 % NP], mp[2 % NP], 0x07050301u) >> 4;
+  for (int p = 0; p < NP; p++) mp[p] = ~(((KP[p] ^ vv) | 0x80008000u) - 0x00010001u);
+  uint32_t oh = hd_perm(mp[1 % NP], mp[0], 0x07050301u) & 0x80808080u;
+  if constexpr (NP == 4) oh |= (hd_perm(mp[3 % NP], mp[2 % NP], 0x07050301u) & 0x80808080u) >> 4;
   const uint32_t t = hd_ctz(oh | 0x80000000u);
   slot = (t >> 3) | ((t & 4u) ^ 4u);
   return oh != 0;
@@ -409,9 +412,16 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
         const bool add = act && !found;
         const bool ins = add && n < CAP;
         sl = found ? sl : n;
-        const uint32_t ishift = (n & 1) * 16;
-#pragma unroll
-        for (int p = 0; p < NP; p++) KP[p] |= (ins && (n >> 1) == (uint32_t)p) ? f << ishift : 0u;
+        // the new key into field n: a 64-bit shift into the pair of dwords
+        // holding fields (n & ~3) .. (n | 3)
+        const uint64_t t64 = (uint64_t)(ins ? f : 0u) << (16 * (n & 3u));
+        const bool lo4 = n < 4;
+        KP[0] |= lo4 ? (uint32_t)t64 : 0u;
+        KP[1 % NP] |= lo4 ? (uint32_t)(t64 >> 32) : 0u;
+        if constexpr (NP == 4) {
+          KP[2 % NP] |= lo4 ? 0u : (uint32_t)t64;
+          KP[3 % NP] |= lo4 ? 0u : (uint32_t)(t64 >> 32);
+        }
         // every processed position is counted; the zeros past the message are
         // taken off below
         cnt += 1ull << (8 * (sl & 7));
@@ -548,13 +558,17 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
       fr += c;
     }
   }
-  uint32_t CT[NP] = {};  // per slot: len << 8 | reversed code
+  uint64_t cc = 0;  // per slot: reversed code (byte k)
+  uint32_t ll = 0;  // per slot: length (nibble k)
 #pragma unroll
   for (int k = 0; k < CAP; k++) {
     const uint32_t L = len[k] - 1;
     const uint32_t code = (uint32_t)(fc64 >> (8 * L)) + crank[k] - ((fr32 >> (4 * L)) & 15u);
     const uint32_t rcode = hd_brev(code) >> (32 - len[k]);
-    CT[k >> 1] |= ((len[k] << 8) | (rcode & 0xFFu)) << (16 * (k & 1));
+    if ((uint32_t)k < n) {
+      cc |= (uint64_t)(rcode & 0xFFu) << (8 * k);
+      ll |= len[k] << (4 * k);
+    }
   }
 
   // the table in canonical order for the emitter
@@ -573,10 +587,9 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
   S.msz = (uint32_t)msz;
   S.lcount = lcount;
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    S.TK[j] = TK[j];
-    S.CT[j] = j < NP ? CT[j < NP ? j : 0] : 0u;
-  }
+  for (int j = 0; j < 4; j++) S.TK[j] = TK[j];
+  S.cc = cc;
+  S.ll = ll;
 #pragma unroll
   for (int j = 0; j < SlotIds<8>::kRegs; j++) S.ids.r[j] = ids.r[j];
   R8_STAMP(4);
@@ -614,9 +627,11 @@ MYYUV_HD void emit_chunk(const EncState& S, int wave_msz, W& bw) {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const int i = i0 + k;
-        const uint32_t ct = (uint32_t)i < S.msz ? rr::f16<8>(S.CT, S.ids.get(i)) : 0u;
-        bits |= (ct & 0xFFu) << nb;
-        nb += ct >> 8;
+        // (every lane looks its code up; past the message the length is 0)
+        const uint32_t sl = S.ids.get(i);
+        const uint32_t len = (uint32_t)i < S.msz ? (S.ll >> (4 * sl)) & 15u : 0u;
+        bits |= ((uint32_t)(S.cc >> (8 * sl)) & ((1u << len) - 1u)) << nb;
+        nb += len;
       }
       bw.put(bits, (int)nb);
     }
@@ -650,8 +665,8 @@ MYYUV_HD void build_single(const CoefRegs& R, EncState& S) {
   S.lcount = 1;
   S.TK[0] = ((uint32_t)R.sym(0) & 0x7FFu) | (1u << 11);
   S.TK[1] = S.TK[2] = S.TK[3] = 0u;
-  S.CT[0] = 1u << 8;  // length 1, code 0
-  S.CT[1] = S.CT[2] = S.CT[3] = 0u;
+  S.cc = 0;  // slot 0: code 0,
+  S.ll = 1;  // length 1
   S.ids.clear();
 }
 

@@ -934,7 +934,7 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
 // K2 over K1's coefficients in HBM: one workgroup per tile (grid (tiles, frames)).
 //   coef: natural-order quads (codec_common.hpp); sizes: [n] u8.
 #ifndef MYYUV_K2_WAVES
-#define MYYUV_K2_WAVES 6  // 6 workgroups of 4 waves per CU: <= 80 VGPRs (20 spilled; A/B against 4 / 5 / 7 / 8: +1.5 % over 5, tools/ab_bench.sh)
+#define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (12 spilled; 6 measured +1.5 % before the emit tables, −1 % after: its spills grew; tools/ab_bench.sh, tools/kus_ab.sh)
 #endif
 __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
                                                          const uint8_t* __restrict__ rmask,
