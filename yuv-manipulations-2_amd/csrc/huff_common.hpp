@@ -349,6 +349,23 @@ MYYUV_HD uint32_t f16(const uint32_t (&a)[CAP / 2], uint32_t i) {
   return d >> ((i & 1) * 16) & 0xFFFFu;
 }
 
+// Ascending sort of CAP (4 or 8) values by a comparator network (19 / 5
+// comparators, each a u32 min and max).
+template <int CAP>
+MYYUV_HD void sort_net(uint32_t (&a)[CAP]) {
+  constexpr int n8[19][2] = {{0, 2}, {1, 3}, {4, 6}, {5, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {0, 1}, {2, 3},
+                             {4, 5}, {6, 7}, {2, 4}, {3, 5}, {1, 4}, {3, 6}, {1, 2}, {3, 4}, {5, 6}};
+  constexpr int n4[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
+  constexpr int nc = CAP == 8 ? 19 : 5;
+#pragma unroll
+  for (int c = 0; c < nc; c++) {
+    const int i = CAP == 8 ? n8[c][0] : n4[c < 5 ? c : 0][0], j = CAP == 8 ? n8[c][1] : n4[c < 5 ? c : 0][1];
+    const uint32_t x = a[i % CAP], y = a[j % CAP];
+    a[i % CAP] = x < y ? x : y;
+    a[j % CAP] = x < y ? y : x;
+  }
+}
+
 }  // namespace rr
 
 // What emit_chunk needs of a block whose code was built (build_r /
@@ -530,19 +547,15 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
 
   R8_STAMP(3);
   // ---------------- 4. canonical order (length, symbol) and codes ----------------
-  uint32_t crank[CAP];
+  // (len, key + 1024) << 4 | slot, unused slots last, sorted by a comparator
+  // network (u32 min / max): rank r's item names its slot, so the codes and
+  // the table are written in rank order
+  uint32_t it[CAP];
 #pragma unroll
-  for (int k = 0; k < CAP; k++) {
-    const uint32_t ck = (len[k] << 11) | (uint32_t)(key[k] + 1024);
-    uint32_t r = 0;
-#pragma unroll
-    for (int j = 0; j < CAP; j++) {
-      if (j == k) continue;
-      const uint32_t cj = (len[j] << 11) | (uint32_t)(key[j] + 1024);
-      r += ((uint32_t)j < n && cj < ck) ? 1u : 0u;
-    }
-    crank[k] = (uint32_t)k < n ? r : 0xFFu;  // unused slots rank nowhere
-  }
+  for (int k = 0; k < CAP; k++)
+    it[k] = (uint32_t)k < n ? ((((len[k] << 11) | (uint32_t)(key[k] + 1024)) << 4) | (uint32_t)k)
+                            : 0xFFFFFFF0u | (uint32_t)k;
+  sort_net<CAP>(it);
   uint64_t fc64 = 0;  // per length: first code
   uint32_t fr32 = 0;            // per length: first canonical rank
   uint32_t table_bytes = 0;
@@ -560,26 +573,17 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
   }
   uint64_t cc = 0;  // per slot: reversed code (byte k)
   uint32_t ll = 0;  // per slot: length (nibble k)
-#pragma unroll
-  for (int k = 0; k < CAP; k++) {
-    const uint32_t L = len[k] - 1;
-    const uint32_t code = (uint32_t)(fc64 >> (8 * L)) + crank[k] - ((fr32 >> (4 * L)) & 15u);
-    const uint32_t rcode = hd_brev(code) >> (32 - len[k]);
-    if ((uint32_t)k < n) {
-      cc |= (uint64_t)(rcode & 0xFFu) << (8 * k);
-      ll |= len[k] << (4 * k);
-    }
-  }
-
-  // the table in canonical order for the emitter
-  uint32_t TK[4] = {0u, 0u, 0u, 0u};
+  uint32_t TK[4] = {0u, 0u, 0u, 0u};  // the table in canonical order: key & 0x7FF | len << 11
 #pragma unroll
   for (int r = 0; r < CAP; r++) {
-    uint32_t kl = 0;  // key & 0x7FF | len << 11 of the symbol ranked r
-#pragma unroll
-    for (int k = 0; k < CAP; k++)
-      kl = crank[k] == (uint32_t)r ? (((uint32_t)key[k] & 0x7FFu) | (len[k] << 11)) : kl;
-    TK[r >> 1] |= kl << (16 * (r & 1));
+    const uint32_t k = it[r] & 15u, ck = it[r] >> 4;
+    const bool used = (uint32_t)r < n;
+    const uint32_t ln = used ? ck >> 11 : 1u, L = ln - 1;
+    const uint32_t code = (uint32_t)(fc64 >> (8 * L)) + (uint32_t)r - ((fr32 >> (4 * L)) & 15u);
+    const uint32_t rcode = hd_brev(code) >> (32 - ln);
+    cc |= (uint64_t)(rcode & 0xFFu) << (8 * (k & 7u));  // (an unused rank names an unused slot)
+    ll |= (used ? ln : 0u) << (4 * (k & 7u));
+    TK[r >> 1] |= ((ck ^ 0x400u) & 0xFFFFu) << (16 * (r & 1));  // key + 1024 -> key & 0x7FF
   }
   S.hdr = nbits | (table_bytes << 16);
   S.size = 3 + table_bytes + (nbits + 7) / 8;
