@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_cli.py tests/test_reference_binding.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03s_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r03s_tests.log; exit 1; }
+tail -2 gpurun_out/r03s_tests.log
+timeout -k 10 300 python3 tools/host_api_rate.py
