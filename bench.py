@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the cpu_baseline sample (0 disables it)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or nproc")
+    ap.add_argument("--events-ctx0", action="store_true",
+                    help="event-stamp K1 on launch group 0 only (default: every group's K1 launches)")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the step without K1's HIP events (no roofline)")
     ap.add_argument("--inflight", type=int, default=3,
@@ -317,10 +319,13 @@ def main():
                 raise SystemExit(f"context {k} frame {b}: device round trip differs from the host-API decode")
 
     # ---- timed region: only K1 (the roofline kernel) is event-stamped, on
-    # context 0's launches (one launch group in nf, spread evenly over the
-    # region): stamping every context's launches costs ~5 % of throughput
+    # every launch group (so the average is over the same launches a
+    # rocprofv3 kernel trace of this run averages), or on launch group 0 only
+    # (--events-ctx0)
+    stamped = codecs[:1] if args.events_ctx0 else codecs
     if not args.no_kernel_events:
-        codecs[0].profile(True, kernels=["fdct_quant"])
+        for c in stamped:
+            c.profile(True, kernels=["fdct_quant"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -357,12 +362,13 @@ def main():
         dist.barrier()
     t = time.perf_counter() - t0
     check_status()
-    frames_ctx0 = args.steps * B  # frames in context 0's (event-stamped) launches
     stats = {}
     if not args.no_kernel_events:
-        for kname, (kms, kn) in codecs[0].kernel_stats().items():
-            stats[kname] = (kms, kn)
-        codecs[0].profile(False)
+        for c in stamped:
+            for kname, (kms, kn) in c.kernel_stats().items():
+                a, n = stats.get(kname, (0.0, 0))
+                stats[kname] = (a + kms, n + kn)
+            c.profile(False)
     # per-kernel breakdown (all kernels stamped, one launch group at a time on
     # one stream), outside the timed region
     breakdown = {}
@@ -434,7 +440,7 @@ def main():
         roof = None
         if k1_n:
             avg_s = k1_ms / k1_n / 1e3
-            alg = round(3 * samples * frames_ctx0 / k1_n)  # a launch covers a batch of frames
+            alg = round(3 * samples * B)  # a launch covers a batch of B frames
             achieved = alg / avg_s / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
