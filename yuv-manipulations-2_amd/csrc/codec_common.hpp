@@ -110,10 +110,14 @@ constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
 #endif
 constexpr uint32_t kWaveEncodeLimit = MYYUV_WAVE_LIMIT;
 constexpr uint32_t kWaveEncodeGrid = 8192;   // waves of k_huff_encode_wave (grid-stride)
-#ifndef MYYUV_WIDE_GRID
-#define MYYUV_WIDE_GRID 1280
+#ifndef MYYUV_WIDE_LANES
+#define MYYUV_WIDE_LANES 64
 #endif
-constexpr uint32_t kWideGrid = MYYUV_WIDE_GRID;  // workgroups of k_huff_encode_wide: 5 per CU fit its LDS
+constexpr uint32_t kWideLanes = MYYUV_WIDE_LANES;  // blocks (lanes) per workgroup of k_huff_encode_wide
+#ifndef MYYUV_WIDE_GRID
+#define MYYUV_WIDE_GRID (1280 * 64 / MYYUV_WIDE_LANES)
+#endif
+constexpr uint32_t kWideGrid = MYYUV_WIDE_GRID;  // workgroups of k_huff_encode_wide: its LDS fits 5 x 64 lanes per CU
 #ifndef MYYUV_K2_GROUP
 #define MYYUV_K2_GROUP 256
 #endif

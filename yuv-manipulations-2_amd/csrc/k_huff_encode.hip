@@ -130,17 +130,17 @@ template <int CAP>
 struct Img {
   uint32_t* base;
   int lane;
-  __device__ __forceinline__ uint32_t& kc(int j) const { return base[(Layout<CAP>::kKC + j) * kWave + lane]; }
-  __device__ __forceinline__ uint32_t& wordAt(int w) const { return base[w * kWave + lane]; }
+  __device__ __forceinline__ uint32_t& kc(int j) const { return base[(Layout<CAP>::kKC + j) * kWideLanes + lane]; }
+  __device__ __forceinline__ uint32_t& wordAt(int w) const { return base[w * kWideLanes + lane]; }
   __device__ __forceinline__ uint8_t& t8(int i) const {
-    return *(reinterpret_cast<uint8_t*>(base) + ((Layout<CAP>::kT + (i >> 2)) * kWave + lane) * 4 + (i & 3));
+    return *(reinterpret_cast<uint8_t*>(base) + ((Layout<CAP>::kT + (i >> 2)) * kWideLanes + lane) * 4 + (i & 3));
   }
   __device__ __forceinline__ uint8_t& sh8(int i) const {
-    return *(reinterpret_cast<uint8_t*>(base) + ((Layout<CAP>::kSH + (i >> 2)) * kWave + lane) * 4 + (i & 3));
+    return *(reinterpret_cast<uint8_t*>(base) + ((Layout<CAP>::kSH + (i >> 2)) * kWideLanes + lane) * 4 + (i & 3));
   }
   __device__ __forceinline__ uint16_t& sh16(int i) const {
     return *reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(base) +
-                                        ((Layout<CAP>::kSH + (i >> 1)) * kWave + lane) * 4 + (i & 1) * 2);
+                                        ((Layout<CAP>::kSH + (i >> 1)) * kWideLanes + lane) * 4 + (i & 1) * 2);
   }
 };
 
@@ -462,9 +462,10 @@ __device__ __forceinline__ bool encode_block(const Img<CAP>& I, const CoefRegs& 
   return true;
 }
 
+template <int W = 64>
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) v = max(v, __shfl_xor(v, d, 64));
+  for (int d = 1; d < W; d <<= 1) v = max(v, __shfl_xor(v, d, W));
   return v;
 }
 
@@ -1075,7 +1076,7 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
 // frames where most blocks overflow): the blocks listed in `work` (count in
 // *work_count), 64 per workgroup; the grid is sized for the worst case, idle
 // groups exit.  Lists of at most `limit` blocks go to k_huff_encode_wave instead.
-__global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict__ coef,
+__global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __restrict__ coef,
                                                         const uint8_t* __restrict__ rmask,
                                                         const uint4* __restrict__ zq, FrameGeom G,
                                                         uint32_t* __restrict__ oslots,
@@ -1085,19 +1086,19 @@ __global__ __launch_bounds__(64) void k_huff_encode_wide(const uint4* __restrict
                                                         const uint32_t* __restrict__ work_count,
                                                         uint32_t limit) {
   constexpr int CAP = 64;
-  __shared__ uint32_t lds[Layout<CAP>::kWords * kWave];
+  __shared__ uint32_t lds[Layout<CAP>::kWords * kWideLanes];
   const uint32_t cnt = *work_count;
   if (cnt <= limit) return;  // short lists: k_huff_encode_wave
-  // grid-stride over 64-block slices of the list (the grid is what the
-  // 32 KB-per-workgroup LDS lets be resident)
-  for (uint32_t base = blockIdx.x * kWave; base < cnt; base += gridDim.x * kWave) {
+  // grid-stride over kWideLanes-block slices of the list (the grid is what
+  // the 512 B-per-lane LDS lets be resident)
+  for (uint32_t base = blockIdx.x * kWideLanes; base < cnt; base += gridDim.x * kWideLanes) {
     const uint32_t i = base + threadIdx.x;
     const bool live = i < cnt;
     const uint32_t g = live ? work[i] : 0;
     CoefRegs R;
     R.load(coef, zq, g, live ? rmask[g] : 0u);
     const int msz = live ? R.msz() : 0;
-    const int wmsz = wave_max(msz);
+    const int wmsz = wave_max<kWideLanes>(msz);
     if (live) {
       const Img<CAP> I{lds, (int)threadIdx.x};
       encode_block<CAP>(I, R, msz, max(wmsz, 1), oslots + (size_t)g * kSlotWords, sizes + g);

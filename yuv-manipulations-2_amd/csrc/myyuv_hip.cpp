@@ -381,8 +381,8 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
                 c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), G, c->oslots.as<uint32_t>(),
                 c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
                 limit);
-  const uint32_t wide = ceil_div(nblk, kWave) < kWideGrid ? ceil_div(nblk, kWave) : kWideGrid;
-  e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(wide), dim3(kWave), s,
+  const uint32_t wide = ceil_div(nblk, kWideLanes) < kWideGrid ? ceil_div(nblk, kWideLanes) : kWideGrid;
+  e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(wide), dim3(kWideLanes), s,
               c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
               c->oslots.as<uint32_t>(), c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list,
               (const uint32_t*)count, limit);
