@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise the FETCH_SIZE / WRITE_SIZE calibration (tools/ubench/calib.hip
-run under rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, tools/r02c.sh) into
+run under rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, tools/runs/r02c.sh) into
 profiles/<tag>_calib.json: per access shape, the known bytes per launch and
 bytes / (counter KiB x 1024) — the factor tools/traffic.py applies to the
 codec kernel with that shape."""
