@@ -109,6 +109,10 @@ constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
 #define MYYUV_WAVE_LIMIT 24576
 #endif
 constexpr uint32_t kWaveEncodeLimit = MYYUV_WAVE_LIMIT;
+#ifndef MYYUV_BATCH_WAVE_LIMIT
+#define MYYUV_BATCH_WAVE_LIMIT 0
+#endif
+constexpr uint32_t kBatchWaveLimit = MYYUV_BATCH_WAVE_LIMIT;  // the same limit for batches (nframes > 1)
 constexpr uint32_t kWaveEncodeGrid = 8192;   // waves of k_huff_encode_wave (grid-stride)
 #ifndef MYYUV_WIDE_LANES
 #define MYYUV_WIDE_LANES 64

@@ -374,7 +374,7 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   const uint32_t nf = G.nframes, nblk = G.cum[3] * nf;
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
-  const uint32_t limit = nf > 1 ? 0u : kWaveEncodeLimit;
+  const uint32_t limit = nf > 1 ? kBatchWaveLimit : kWaveEncodeLimit;
   int e = 0;
   if (limit > 0)
     e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
