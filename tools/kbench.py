@@ -6,6 +6,7 @@ compress_device + decompress_device, per-kernel HIP-event times.
   MYYUV_HIP_LIB=<dir>/libmyyuv_hip.so python3 tools/kbench.py [steps] [WxH]
 
 WxH: a tiled synthetic frame of that size (SURVEY.md §8d generator) instead.
+KB_Q=90: quality for all three planes (default 50).
 """
 import os
 import sys
@@ -22,8 +23,9 @@ def main():
     import myyuv_hip
     from oracle import oracle as O
     g = myyuv_file.YUVFile.load(os.path.join(ROOT, "tests", "golden", "chef-with-trumpet-big-DCT-50.myyuv"))
-    w, h, q = g.width, g.height, (50, 50, 50)
+    w, h = g.width, g.height
     raw = O.decompress(g.data, w, h, tuple(g.params))
+    q = (int(os.environ.get("KB_Q", "50")),) * 3
     if len(sys.argv) > 2:
         import synth
         ws, hs = w, h
@@ -51,7 +53,7 @@ def main():
             rc = repr(e)
     stats = codec.kernel_stats()
     ok = bytes(d_out.cpu().numpy()) == expect
-    print(f"{os.environ.get('MYYUV_HIP_LIB', 'default')} {w}x{h}: rc={rc} roundtrip_equal={ok}")
+    print(f"{os.environ.get('MYYUV_HIP_LIB', 'default')} {w}x{h} q{q[0]}: rc={rc} roundtrip_equal={ok}")
     for k, (ms, n) in stats.items():
         if n:
             print(f"  {k:14s} {ms / n * 1e3:9.2f} us")

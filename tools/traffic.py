@@ -71,6 +71,8 @@ def main(tag):
                   "hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
                   "read_factor": rf, "write_factor": wf,
                   "hbm_bytes_per_launch": int(rd + wr), "avg_ns": durations.get(k)}
+        if durations.get(k):
+            out[k]["hbm_gb_per_s"] = round((rd + wr) / durations[k], 1)
     with open(os.path.join(dst, f"{tag}_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
