@@ -138,22 +138,28 @@ def launch_selftest():
     dist.destroy_process_group()
 
 
-def load_traffic():
-    """Per-launch HBM bytes of K1 from the newest profiles/*traffic*.json."""
+def load_traffic(frame, batch):
+    """Per-launch HBM bytes of K1 (calibrated FETCH_SIZE / WRITE_SIZE) from the
+    newest profile of this bench workload (profiles/*_traffic.json written by
+    tools/traffic.py from a tools/profile.sh run, which records the profiled
+    frame and launch-group size), scaled to `batch` frames per launch."""
     pdir = os.path.join(ROOT, "profiles")
-    best = None
-    if os.path.isdir(pdir):
-        for n in sorted(os.listdir(pdir)):
-            if n.endswith(".json") and "traffic" in n:
-                best = os.path.join(pdir, n)
-    if not best:
+    if not os.path.isdir(pdir):
         return None
-    try:
-        with open(best) as f:
-            d = json.load(f)
-        return d.get("fdct_quant", {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+    found = None
+    for n in sorted(os.listdir(pdir)):
+        if not n.endswith("_traffic.json"):
+            continue
+        try:
+            with open(os.path.join(pdir, n)) as f:
+                d = json.load(f)
+            b = d.get("_bench") or {}
+            v = d.get("fdct_quant", {}).get("hbm_bytes_per_launch")
+            if b.get("frame") == frame and b.get("frames_per_launch") and v:
+                found = v * batch // b["frames_per_launch"]
+        except Exception:
+            continue
+    return found
 
 
 def cpu_model():
@@ -444,7 +450,7 @@ def main():
             achieved = alg / avg_s / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": load_traffic(), "kernel": "fdct_quant",
+                    "traffic": load_traffic(f"{w}x{h}", B), "kernel": "fdct_quant",
                     "algorithmic_bytes_per_launch": alg, "avg_launch_us": round(avg_s * 1e6, 2)}
         kernel_us = {k: round(kms / kn * 1e3, 2) for k, (kms, kn) in breakdown.items() if kn}
         # the same K1 figure with one launch group at a time (the untimed

@@ -155,3 +155,16 @@ def test_bench_rejects_rank_count_mismatch():
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode != 0
     assert "--gpus 2 but the launcher started 3 ranks" in r.stderr
+
+
+def test_bench_traffic_matches_its_workload():
+    """roofline.traffic comes from a profile of the bench's own frame, scaled
+    to the bench's launch-group size (not from another workload's profile)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    t7 = bench.load_traffic("4032x3008", 7)
+    assert t7 is not None and t7 > 0
+    assert abs(bench.load_traffic("4032x3008", 14) - 2 * t7) <= 1
+    assert bench.load_traffic("17x3", 7) is None

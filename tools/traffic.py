@@ -73,6 +73,13 @@ def main(tag):
                   "hbm_bytes_per_launch": int(rd + wr), "avg_ns": durations.get(k)}
         if durations.get(k):
             out[k]["hbm_gb_per_s"] = round((rd + wr) / durations[k], 1)
+    # the bench run profiled (tools/profile.sh): its frame and launch-group
+    # size, so bench.py can scale the per-launch bytes to its own groups
+    bj = os.path.join(src, "bench_trace.json")
+    if os.path.exists(bj):
+        with open(bj) as f:
+            cfg = json.loads(f.read().strip().splitlines()[-1])["config"]
+        out["_bench"] = {"frame": cfg["frame"], "frames_per_launch": cfg["frames_per_launch"]}
     with open(os.path.join(dst, f"{tag}_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
