@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=7,
                     help="frames per launch (the batch entry points): each kernel covers this "
                          "many frames")
+    ap.add_argument("--stream-priority", default="",
+                    help="comma-separated HIP stream priorities of the launch groups' streams "
+                         "(cycled; default all normal)")
     ap.add_argument("--gather-chunk", type=int, default=32,
                     help="N>1: frames per chunk of the overlapped gather to rank 0")
     ap.add_argument("--no-side", action="store_true",
@@ -271,7 +274,10 @@ def main():
     frames = args.steps * per_step
     # explicit streams: the null stream's handle is 0, which the C ABI reads as
     # "the context's own stream" (the N>1 gather's events must see the launches)
-    streams = [torch.cuda.Stream(dev) for _ in range(nf)]
+    # --stream-priority: per launch group, a HIP stream priority (0 normal,
+    # negative higher), cycled over the groups in flight
+    prios = [int(v) for v in args.stream_priority.split(",")] if args.stream_priority else [0]
+    streams = [torch.cuda.Stream(dev, priority=prios[k % len(prios)]) for k in range(nf)]
     sps = [st.cuda_stream for st in streams]
     cap = (cap + 3) & ~3  # payload slots of a batch are dword aligned
     # distinct input copies (HBM-resident, more than the Infinity Cache holds);
