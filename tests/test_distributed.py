@@ -2,6 +2,7 @@
 per rank, streams gathered to rank 0 in frame order (yuv-manipulations-2_amd/
 batch.py).  The codec here is the CPU restatement; on the GPU box the same
 driver runs with the HIP codec over RCCL."""
+import json
 import os
 import socket
 
@@ -168,3 +169,37 @@ def test_bench_traffic_matches_its_workload():
     assert t7 is not None and t7 > 0
     assert abs(bench.load_traffic("4032x3008", 14) - 2 * t7) <= 1
     assert bench.load_traffic("17x3", 7) is None
+
+
+def _bench_json(stdout):
+    line = [ln for ln in stdout.splitlines() if ln.startswith("{")][-1]
+    return json.loads(line)
+
+
+@pytest.mark.parametrize("workload,extra", [
+    ("batch4k", ["--frames", "4", "--batch", "1", "--inflight", "2", "--gather-chunk", "1", "--steps", "2"]),
+    ("chef-big", ["--batch", "1", "--inflight", "2", "--gather-chunk", "1", "--steps", "1", "--input-frames", "2"]),
+])
+def test_bench_n2_loop_cpu_codec(workload, extra):
+    """bench.py's own N > 1 loop end to end at world 2 (gloo), with the CPU
+    restatement standing in for the HIP codec (--cpu-codec): the frames dealt
+    round-robin, launch groups over two contexts, the chunked gather of every
+    rank's streams to rank 0 inside the timed region, and rank 0's checks of
+    what it gathered (batch4k: every frame of the first and last step against
+    tests/golden/batch4k_512.json; chef-big: the pinned reference bytes)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-codec",
+                        "--workload", workload, "--warmup", "1"] + extra,
+                       capture_output=True, text=True, timeout=600, env=_bench_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _bench_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["scaling"] == ("strong" if workload == "batch4k" else "weak")
+    steps = d["steps"]
+    per = d["config"]["frames_per_step_per_gpu"]
+    assert d["config"]["frames_per_step"] == 2 * per
+    assert f"rank 0 gathered {2 * steps * per} streams" in d["verified"]["gathered"]
+    assert "first_pass" in d["verified"]
+    if workload == "batch4k":
+        assert "tests/golden/batch4k_512.json" in d["verified"]["gathered"]

@@ -99,40 +99,49 @@ def test_batch_4k_shifted_origins(codec, oracle, chef_big):
             assert np.abs(got[a:b].astype(int) - want[a:b].astype(int)).max() == 0, i
 
 
-def test_batch_4k_64_distinct_frames_gathered(codec, oracle, chef_big):
-    """configs[3]/[4] at world size 1: 64 distinct 3840x2160 tiled frames with
-    the §8(d) per-frame origins (796 MB of input, more than the Infinity
-    Cache), compressed in four 16-frame launches through the batch device
-    entry point, the streams collected by bench.py's overlapped gather
-    (batch.ChunkedGather over RCCL, world 1), decoded in 16-frame launches.
-    Every stream equals the oracle's, frame 0 (origin 0) is SURVEY's pinned
-    file, and every plane decodes with max-abs-diff 0 against the oracle."""
+def test_batch4k_512_frames_gathered(codec, oracle, chef_big):
+    """BASELINE configs[3]/[4] at full size on one GPU (world size 1): the 512
+    distinct 3840x2160 frames of SURVEY.md §8(d) (per-frame shifted origins,
+    6.4 GB of input built in HBM by synth.tiled_frame_torch), compressed in
+    32-frame launches through the batch device entry point, the streams
+    collected by bench.py's overlapped gather (batch.ChunkedGather over RCCL),
+    decoded in 32-frame launches.  Every input, stream and decode equals
+    tests/golden/batch4k_512.json (the oracle's sha256 per frame, made by
+    tests/golden/make_batch4k.py); frame 0 is SURVEY's pinned file
+    (f7de6788...); 8 frames spread over the batch decode with per-plane
+    max-abs-diff 0 against the oracle's decode."""
+    import json
     import os
     import socket
+    from concurrent.futures import ThreadPoolExecutor
     import torch
     import torch.distributed as dist
     import batch
     import myyuv_file
-    import myyuv_hip
     import synth
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "batch4k_512.json")) as fh:
+        man = json.load(fh)["frames"]
     f, raw = chef_big
-    w, h, nf, per, q = 3840, 2160, 64, 16, (50, 50, 50)
-    frames = []
-    for i in range(nf):
-        ox, oy = synth.batch_origin(i, f.width, f.height)
-        frames.append(synth.tiled_frame(raw, f.width, f.height, w, h, ox, oy).tobytes())
-    assert sha(myyuv_file.YUVFile(width=w, height=h, data=frames[0]).dumps()) == \
-        "d578631d41859dcd4b94de5784a9435a638c8127e478a062db47f13804455127"
-    assert len(set(frames)) == nf
+    w, h, nf, per, q = 3840, 2160, 512, 32, (50, 50, 50)
+    cap = 4 << 20  # the largest stream is 2,471,404 B; capacity is checked on device
     dev = torch.device("cuda", 0)
     fb = w * h * 3 // 2
-    cap = (myyuv_hip.payload_bound(w, h) + 3) & ~3
-    d_in = torch.empty(nf * fb, dtype=torch.uint8, device=dev)
+    src = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+    d_in = torch.empty((nf, fb), dtype=torch.uint8, device=dev)
     for i in range(nf):
-        d_in[i * fb:(i + 1) * fb] = torch.frombuffer(bytearray(frames[i]), dtype=torch.uint8).to(dev)
+        ox, oy = synth.batch_origin(i, f.width, f.height)
+        d_in[i] = synth.tiled_frame_torch(src, f.width, f.height, w, h, ox, oy)
+
+    def shas(t, n, stride):
+        flat = t.reshape(-1)
+        with ThreadPoolExecutor(8) as ex:
+            return list(ex.map(lambda i: sha(flat[i * stride:(i + 1) * stride].cpu().numpy().tobytes()), range(n)))
+
+    assert shas(d_in, nf, fb) == [m["input_sha"] for m in man]
     d_pay = torch.empty((nf, cap), dtype=torch.uint8, device=dev)
     d_sz = torch.zeros(nf, dtype=torch.int32, device=dev)
-    d_out = torch.empty(nf * fb, dtype=torch.uint8, device=dev)
+    d_out = torch.empty((nf, fb), dtype=torch.uint8, device=dev)
     # an explicit stream: the null stream's handle is 0, which the C ABI reads
     # as "the context's own stream", and the gather's events must see the
     # launches
@@ -148,7 +157,7 @@ def test_batch_4k_64_distinct_frames_gathered(codec, oracle, chef_big):
     try:
         gat = batch.ChunkedGather(dist, 1, 0, dev)
         for c0 in range(0, nf, per):
-            codec.compress_batch_device(d_in[c0 * fb].data_ptr(), per, w, h, q, d_pay[c0].data_ptr(), cap,
+            codec.compress_batch_device(d_in[c0].data_ptr(), per, w, h, q, d_pay[c0].data_ptr(), cap,
                                         d_sz[c0:c0 + per].data_ptr(), sp)
             ev = torch.cuda.Event()
             ev.record(st)
@@ -161,20 +170,20 @@ def test_batch_4k_64_distinct_frames_gathered(codec, oracle, chef_big):
     assert rc == 0, (rc, bad)
     for c0 in range(0, nf, per):
         codec.decompress_batch_device(d_pay[c0].data_ptr(), d_sz[c0:c0 + per].data_ptr(), cap, per, w, h, q,
-                                      d_out[c0 * fb].data_ptr(), sp)
+                                      d_out[c0].data_ptr(), sp)
     rc, bad = codec.sync_status(sp)
     assert rc == 0, (rc, bad)
     assert len(got) == nf
     sizes = d_sz.cpu().tolist()
-    pay0 = bytes(got[0].cpu().numpy())
-    assert len(pay0) == 2155708
-    assert sha(myyuv_file.YUVFile(width=w, height=h, data=frames[0]).compressed(b"222", pay0).dumps()) == \
+    assert sizes == [m["payload_size"] for m in man]
+    pays = [bytes(t.cpu().numpy()) for t in got]
+    assert [sha(p) for p in pays] == [m["payload_sha"] for m in man]
+    img0 = myyuv_file.YUVFile(width=w, height=h, data=bytes(d_in[0].cpu().numpy()))
+    assert sha(img0.compressed(b"222", pays[0]).dumps()) == \
         "f7de6788c9c7574eeb145689a55936f2d5f9d9e4740e6d70198b9976298d5d31"
-    for i in range(nf):
-        pay = bytes(got[i].cpu().numpy())
-        assert len(pay) == sizes[i], i
-        assert pay == oracle.compress(frames[i], w, h, q), i
-        gd = np.frombuffer(bytes(d_out[i * fb:(i + 1) * fb].cpu().numpy()), np.uint8)
-        want = np.frombuffer(oracle.decompress(pay, w, h, q), np.uint8)
+    assert shas(d_out, nf, fb) == [m["decoded_sha"] for m in man]
+    for i in (0, 1, 63, 128, 255, 256, 400, 511):
+        gd = d_out[i].cpu().numpy()
+        want = np.frombuffer(oracle.decompress(pays[i], w, h, q), np.uint8)
         for a, b in ((0, w * h), (w * h, w * h * 5 // 4), (w * h * 5 // 4, fb)):  # Y, U, V
             assert np.abs(gd[a:b].astype(int) - want[a:b].astype(int)).max() == 0, i

@@ -2,6 +2,7 @@
 when oracle/_ref was built from the reference sources, against the reference
 library itself.  No GPU needed."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -230,3 +231,38 @@ def test_noise_4k_known_answer(oracle):
     pay = oracle.compress(n, 3840, 2160, (50, 50, 50))
     assert len(pay) == 9613725
     assert sha(img.compressed(b"222", pay).dumps()).startswith("88ba856a")
+
+
+@pytest.mark.parametrize("f", [0, 1, 300, 511])
+def test_batch4k_manifest(oracle, chef_big, f):
+    """tests/golden/batch4k_512.json (BASELINE configs[3]/[4], made by
+    tests/golden/make_batch4k.py): frame f's generated input, its q50 stream
+    and its decode agree with the oracle here; frame 0 is SURVEY.md §8(d)'s
+    pinned tiled 4K file (f7de6788...).  The torch generator the bench and
+    the GPU test use equals the numpy one."""
+    import hashlib
+    import json
+    import torch
+    import myyuv_file
+    import synth
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "batch4k_512.json")) as fh:
+        man = json.load(fh)
+    assert man["frames_total"] == len(man["frames"]) == 512 and man["quality"] == 50
+    m = man["frames"][f]
+    g, raw = chef_big
+    ox, oy = synth.batch_origin(f, g.width, g.height)
+    assert m["f"] == f and m["origin"] == [ox, oy]
+    px = synth.tiled_frame(raw, g.width, g.height, 3840, 2160, ox, oy).tobytes()
+    tpx = synth.tiled_frame_torch(torch.frombuffer(bytearray(raw), dtype=torch.uint8), g.width, g.height,
+                                  3840, 2160, ox, oy)
+    assert bytes(tpx.numpy()) == px
+    sha = lambda b: hashlib.sha256(b).hexdigest()  # noqa: E731
+    assert sha(px) == m["input_sha"]
+    pay = oracle.compress(px, 3840, 2160, (50, 50, 50))
+    assert len(pay) == m["payload_size"] and sha(pay) == m["payload_sha"]
+    assert sha(oracle.decompress(pay, 3840, 2160, (50, 50, 50))) == m["decoded_sha"]
+    if f == 0:
+        img = myyuv_file.YUVFile(width=3840, height=2160, data=px)
+        assert sha(img.compressed(b"222", pay).dumps()) == \
+            "f7de6788c9c7574eeb145689a55936f2d5f9d9e4740e6d70198b9976298d5d31"

@@ -146,6 +146,14 @@ constexpr uint32_t kWaveRun = kWave * kMaxChunk;
 constexpr uint32_t kTInfoWords = 16;
 constexpr uint32_t kTInfoPrefix = 8;
 constexpr uint16_t kSrcOverflow = 0xFFFF;
+// The hand-off is laid out for exactly four K2 waves per tile: k_tile_scan sums
+// tinfo words 1..4, k_stream_out keeps four run totals, k_encode_tile's
+// phase 1 covers 4 waves x 4 units x 16 blocks, and tinfo word kTInfoPrefix
+// must lie past the run words; a tile's byte offsets must fit srcoff's u16
+// below kSrcOverflow.
+static_assert(kK2Group == 4 * kWave, "the K2 -> K4 hand-off assumes 4 waves per tile");
+static_assert(1 + kK2Group / kWave <= kTInfoPrefix, "tinfo run words overlap the tile prefix");
+static_assert(kTileCap <= kSrcOverflow, "tile offsets must fit the u16 srcoff below kSrcOverflow");
 
 // Plane, first block (frame-local) and block count of tile t of a frame.
 __host__ __device__ __forceinline__ int tile_plane(const FrameGeom& G, uint32_t t) {

@@ -24,7 +24,15 @@ __device__ __forceinline__ constexpr int tix(int i, int j) { return (i >> 1) * 1
 
 __device__ __forceinline__ uint32_t bits(float x) { return __builtin_bit_cast(uint32_t, x); }
 
-__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+// Hand-off between a wave's lanes through LDS: a wave's LDS accesses execute
+// in program order, so no wait is needed, but the compiler must not move LDS
+// stores and loads across this point (wave-scope release/acquire: no
+// instructions, a compiler memory barrier).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Keeps 16 accumulators' updates in round-robin order (the scheduler would
 // otherwise serialise them chain by chain to save registers).

@@ -171,6 +171,27 @@ class Codec:
             raise CodecError(rc, bad.value)
         return out.tobytes()
 
+    def compress_into(self, iyuv, w, h, q, out):
+        """IYUV numpy buffer -> payload written into the caller's numpy buffer
+        `out` (no per-call allocation); returns the payload size."""
+        size = ctypes.c_uint32(0)
+        rc = load().myyuv_gpu_dct_compress(self._h, _u8(iyuv), w, h, _u8(_q(q)), _u8(out), out.size,
+                                           ctypes.byref(size))
+        if rc:
+            raise CodecError(rc)
+        return size.value
+
+    def decompress_into(self, payload, w, h, q, out):
+        """payload numpy buffer -> IYUV frame written into the caller's numpy
+        buffer `out` (W*H*3/2 bytes)."""
+        if out.size < w * h * 3 // 2:
+            raise ValueError("output smaller than W*H*3/2")
+        bad = ctypes.c_int64(-1)
+        rc = load().myyuv_gpu_dct_decompress(self._h, _u8(payload), payload.size, w, h, _u8(_q(q)), _u8(out),
+                                             ctypes.byref(bad))
+        if rc:
+            raise CodecError(rc, bad.value)
+
     def compress_batch(self, frames, w, h, q):
         """Host-buffer batch: a list of IYUV frames of one geometry -> their
         DCTYUV payloads (one launch per kernel for the batch)."""

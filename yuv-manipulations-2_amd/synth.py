@@ -44,3 +44,22 @@ def tiled_frame(src_iyuv, ws, hs, w, h, ox=0, oy=0):
 
 def batch_origin(f, ws, hs):
     return (f * 8) % ws, (f * 8) % hs
+
+
+def tiled_frame_torch(src, ws, hs, w, h, ox=0, oy=0):
+    """tiled_frame on src's device: src is a uint8 tensor holding the ws x hs
+    IYUV frame; returns the w x h IYUV frame as a flat uint8 tensor (the
+    bench and the GPU tests build the 512-frame batch in HBM this way)."""
+    import torch
+    dev = src.device
+    y = src[: ws * hs].view(hs, ws)
+    u = src[ws * hs: ws * hs * 5 // 4].view(hs // 2, ws // 2)
+    v = src[ws * hs * 5 // 4: ws * hs * 3 // 2].view(hs // 2, ws // 2)
+
+    def tile(p, pw, ph, ox, oy):
+        rows = (torch.arange(ph, device=dev) + oy) % p.shape[0]
+        cols = (torch.arange(pw, device=dev) + ox) % p.shape[1]
+        return p.index_select(0, rows).index_select(1, cols).reshape(-1)
+
+    return torch.cat([tile(y, w, h, ox, oy), tile(u, w // 2, h // 2, ox // 2, oy // 2),
+                      tile(v, w // 2, h // 2, ox // 2, oy // 2)])
