@@ -155,15 +155,6 @@ static_assert(kK2Group == 4 * kWave, "the K2 -> K4 hand-off assumes 4 waves per 
 static_assert(1 + kK2Group / kWave <= kTInfoPrefix, "tinfo run words overlap the tile prefix");
 static_assert(kTileCap <= kSrcOverflow, "tile offsets must fit the u16 srcoff below kSrcOverflow");
 
-// Row mask (bit r: row r has a nonzero coefficient) of a block's 8-byte
-// nonzero map (K1; byte r = row r): per dword, bit 7 of each byte set when the
-// byte is nonzero, then the four flags gathered into bits 0..3.
-__host__ __device__ __forceinline__ uint32_t rowmask4(uint32_t x) {
-  const uint32_t f = ((((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u);
-  return ((f >> 7) | (f >> 14) | (f >> 21) | (f >> 28)) & 0xFu;
-}
-__host__ __device__ __forceinline__ uint32_t rowmask_of(uint2 m) { return rowmask4(m.x) | (rowmask4(m.y) << 4); }
-
 // Plane, first block (frame-local) and block count of tile t of a frame.
 __host__ __device__ __forceinline__ int tile_plane(const FrameGeom& G, uint32_t t) {
   return t >= G.tcum[1] ? (t >= G.tcum[2] ? 2 : 1) : 0;

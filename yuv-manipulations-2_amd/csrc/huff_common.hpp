@@ -648,39 +648,13 @@ MYYUV_HD void emit_chunk(const EncState& S, int wave_msz, W& bw) {
 //   for sure (nonzero coefficients, plus one for a zero inside the message);
 //   r8x: the rest, encode_block_r<8> with the overflow worklist behind it.
 constexpr uint32_t kClassSingle = 0, kClassR4 = 1, kClassR8 = 2, kClassR8x = 3, kClassDead = 4;
-// from the message length msz and the nonzero count nnz
-MYYUV_HD uint32_t class_of(int msz, uint32_t nnz) {
-  if (msz <= 1) return kClassSingle;
-  const uint32_t nub = nnz + ((uint32_t)msz > nnz ? 1u : 0u);
-  return nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
-}
 MYYUV_HD uint32_t block_class(const CoefRegs& R, int msz) {
+  if (msz <= 1) return kClassSingle;
   uint32_t nnz = 0;
 #pragma unroll
   for (int w = 0; w < 32; w++) nnz += ((R.w[w] & 0xFFFFu) != 0) + ((R.w[w] >> 16) != 0);
-  return class_of(msz, nnz);
-}
-
-// Message length from a block's nonzero map (K1's 8 bytes, byte r = row r,
-// bit c = column c): zig-zag indices grow with the anti-diagonal r + c, so
-// along a row they grow with c, and msz = 1 + the largest zig-zag index of a
-// nonzero coefficient is the maximum over rows of a per-(row, pattern) value:
-// MszTab::v[r * 256 + pattern] (0 for an empty row).
-struct MszTab {
-  uint8_t v[8 * 256];
-};
-constexpr MszTab make_msz_tab() {
-  MszTab t{};
-  uint8_t inv[64] = {};
-  for (int i = 0; i < 64; i++) inv[c_zz[i]] = (uint8_t)i;
-  for (int r = 0; r < 8; r++)
-    for (int b = 0; b < 256; b++) {
-      int m = 0;
-      for (int c = 0; c < 8; c++)
-        if (((b >> c) & 1) && inv[r * 8 + c] + 1 > m) m = inv[r * 8 + c] + 1;
-      t.v[r * 256 + b] = (uint8_t)m;
-    }
-  return t;
+  const uint32_t nub = nnz + ((uint32_t)msz > nnz ? 1u : 0u);
+  return nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
 }
 
 // Blocks whose message is one symbol (msz <= 1: all zero, or the DC

@@ -565,7 +565,7 @@ __device__ __forceinline__ void put_bits(uint32_t* img, uint32_t off, uint32_t v
   if (sh + nb > 32) atomicOr(&img[w + 1], v >> (32 - sh));
 }
 
-__device__ void encode_block_wave(const uint4* __restrict__ coef, const uint2* __restrict__ nzm, uint32_t g,
+__device__ void encode_block_wave(const uint4* __restrict__ coef, const uint8_t* __restrict__ rmask, uint32_t g,
                                   uint32_t* img,
                                   uint32_t* __restrict__ oslots, uint8_t* __restrict__ sizes,
                                   uint32_t* __restrict__ tile_bytes,
@@ -577,13 +577,12 @@ __device__ void encode_block_wave(const uint4* __restrict__ coef, const uint2* _
   WSTAMP(0);
   // ---- lane i: zig-zag position i (Huffman.cpp:176-182)
   const uint32_t nat = c_zz_lane[lane];
-  const uint2 nm = nzm[g];
-  const uint32_t word = (((nat >> 3) < 4 ? nm.x : nm.y) >> (8 * ((nat >> 3) & 3u))) & 0xFFu  // row nat >> 3 is nonzero
+  const uint32_t word = (rmask[g] >> (nat >> 3)) & 1u  // row nat >> 3 is nonzero
                             ? reinterpret_cast<const uint32_t*>(coef)[coef_quad(g, nat >> 3) * 4u + ((nat >> 1) & 3u)]
                             : 0u;
   const int v = (int)(int16_t)(word >> (16 * (nat & 1)));
-  const uint64_t nzb = __ballot(v != 0);
-  int msz = nzb ? 64 - __clzll((long long)nzb) : 0;
+  const uint64_t nzm = __ballot(v != 0);
+  int msz = nzm ? 64 - __clzll((long long)nzm) : 0;
   if (msz == 0) msz = 1;  // all-zero block: one symbol 0 (Huffman.cpp:191-194)
   const bool act = lane < (uint32_t)msz;
   const bool has_zero = __ballot(act && v == 0) != 0;
@@ -727,7 +726,7 @@ __device__ void encode_block_wave(const uint4* __restrict__ coef, const uint2* _
 // encode_block_wave); exits at once when the list is long (the lane pass
 // k_huff_encode_wide takes it).
 __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict__ coef,
-                                                        const uint2* __restrict__ nzm, FrameGeom G,
+                                                        const uint8_t* __restrict__ rmask, FrameGeom G,
                                                         uint32_t* __restrict__ oslots,
                                                         uint8_t* __restrict__ sizes,
                                                         uint32_t* __restrict__ tinfo,
@@ -739,7 +738,7 @@ __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict
   if (cnt > limit) return;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
     const uint32_t g = work[i];
-    encode_block_wave(coef, nzm, g, img, oslots, sizes, tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, i);
+    encode_block_wave(coef, rmask, g, img, oslots, sizes, tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, i);
   }
 }
 
@@ -749,29 +748,12 @@ namespace {
 // the tile's LDS image (k_encode_tile: row c of the tile's block b at
 // c * kK2Group + b), which also hands the overflow blocks' coefficients to the
 // overflow passes through HBM.
-__constant__ MszTab c_msz_tab = make_msz_tab();
-
 struct GlobalCoef {
   const uint4* coef;
-  const uint2* nzm;   // K1's nonzero maps, 8 B per block
-  const uint8_t* tab; // MszTab staged in LDS
+  const uint8_t* rmask;
   const uint4* zq;
   uint32_t gb;  // batch-global index of the tile's block 0
-  // row mask, message length and class of the tile's block b from K1's
-  // nonzero map alone: the coefficients are loaded once, after the sort
-  __device__ __forceinline__ void classify(uint32_t b, uint32_t& rm, int& msz, uint32_t& cls) const {
-    const uint2 m = nzm[gb + b];
-    uint32_t ms = 0, mk = 0;
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      const uint32_t v = tab[r * 256 + (((r < 4 ? m.x : m.y) >> (8 * (r & 3))) & 0xFFu)];
-      ms = max(ms, v);
-      mk |= min(v, 1u) << r;  // (nonzero exactly when the row is)
-    }
-    rm = mk;
-    msz = (int)ms;
-    cls = class_of(msz, (uint32_t)(__popc(m.x) + __popc(m.y)));
-  }
+  __device__ __forceinline__ uint32_t rm(uint32_t b) const { return rmask[gb + b]; }
   __device__ __forceinline__ void load(CoefRegs& R, uint32_t b, uint32_t m) const { R.load(coef, zq, gb + b, m); }
   __device__ __forceinline__ void spill(const CoefRegs&, uint32_t, uint32_t) const {}
 };
@@ -781,16 +763,9 @@ struct LdsCoefT {
   const uint4* img;
   const uint8_t* s_rm;
   uint4* coef;
-  uint2* nzm;
+  uint8_t* rmask;
   uint32_t gb;
-  // (the tile's coefficients are in LDS: classified from the image itself)
-  __device__ __forceinline__ void classify(uint32_t b, uint32_t& rm, int& msz, uint32_t& cls) const {
-    rm = s_rm[b];
-    CoefRegs R;
-    load(R, b, rm);
-    msz = R.msz();
-    cls = block_class(R, msz);
-  }
+  __device__ __forceinline__ uint32_t rm(uint32_t b) const { return s_rm[b]; }
   __device__ __forceinline__ void load(CoefRegs& R, uint32_t b, uint32_t m) const {
 #pragma unroll
     for (int c = 0; c < 8; c++) {
@@ -801,18 +776,14 @@ struct LdsCoefT {
       R.w[4 * c + 3] = v.w;
     }
   }
-  // a block for the overflow passes: its nonzero rows and nonzero map to HBM (K1's layout)
+  // a block for the overflow passes: its nonzero rows and row mask to HBM (K1's layout)
   __device__ __forceinline__ void spill(const CoefRegs& R, uint32_t b, uint32_t m) const {
     if (!kSpill) return;
     const uint32_t g = gb + b;
 #pragma unroll
     for (int c = 0; c < 8; c++)
       if ((m >> c) & 1u) coef[coef_quad(g, c)] = make_uint4(R.w[4 * c], R.w[4 * c + 1], R.w[4 * c + 2], R.w[4 * c + 3]);
-    uint32_t mp[2] = {0u, 0u};  // bit n = coefficient n (natural order) nonzero
-#pragma unroll
-    for (int w = 0; w < 32; w++)
-      mp[w >> 4] |= (((R.w[w] & 0xFFFFu) != 0u ? 1u : 0u) | ((R.w[w] >> 16) != 0u ? 2u : 0u)) << (2 * (w & 15));
-    nzm[g] = make_uint2(mp[0], mp[1]);
+    rmask[g] = (uint8_t)m;
   }
 };
 
@@ -855,7 +826,13 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
   uint32_t cls = kClassDead;
   int msz = 0;
   uint32_t rm = 0;
-  if (tid < nloc) src.classify(tid, rm, msz, cls);
+  if (tid < nloc) {
+    rm = src.rm(tid);
+    CoefRegs R;
+    src.load(R, tid, rm);
+    msz = R.msz();
+    cls = block_class(R, msz);
+  }
   // ---- counting sort by class (stable: class, then wave, then lane)
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t rank = 0;
@@ -961,7 +938,7 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
 #define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (12 spilled; 6 measured +1.5 % before the emit tables, −1 % after: its spills grew; tools/ab_bench.sh, tools/kus_ab.sh)
 #endif
 __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
-                                                         const uint16_t* __restrict__ nzm,
+                                                         const uint8_t* __restrict__ rmask,
                                                          const uint4* __restrict__ zq, FrameGeom G,
                                                          uint32_t* __restrict__ stage,
                                                          uint32_t* __restrict__ tinfo,
@@ -970,16 +947,11 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
                                                          uint32_t* __restrict__ work,
                                                          uint32_t* __restrict__ work_count) {
   __shared__ TileScratch sc;
-  __shared__ uint2 s_tab[sizeof(MszTab) / 8];
-  static_assert(sizeof(MszTab) / 8 == kK2Group, "one 8-byte piece of the msz table per thread");
-  s_tab[threadIdx.x] = reinterpret_cast<const uint2*>(&c_msz_tab)[threadIdx.x];
-  __syncthreads();
   const uint32_t t = blockIdx.x, f = blockIdx.y;
   const int p = tile_plane(G, t);
   const uint32_t g0 = tile_first(G, p, t);
   const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
-  const GlobalCoef src{coef, reinterpret_cast<const uint2*>(nzm), reinterpret_cast<const uint8_t*>(s_tab), zq,
-                       f * G.cum[3] + g0};
+  const GlobalCoef src{coef, rmask, zq, f * G.cum[3] + g0};
   encode_tile(src, sc, f * G.tcum[3] + t, nloc, stage, tinfo, sizes, srcoff, work, work_count);
 }
 
@@ -1049,7 +1021,7 @@ __device__ __forceinline__ void load_tile_rows(const uint8_t* __restrict__ frame
 __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __restrict__ frame, FrameGeom G,
                                                              const QTables* __restrict__ qt,
                                                              uint4* __restrict__ coef,
-                                                             uint2* __restrict__ nzm,
+                                                             uint8_t* __restrict__ rmask,
                                                              uint32_t* __restrict__ stage,
                                                              uint32_t* __restrict__ tinfo,
                                                              uint8_t* __restrict__ sizes,
@@ -1084,9 +1056,8 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
     uint32_t c[16];
     fdct_core(img, tb, q, s_q, p, c);
     uint4 lo, hi;
-    uint32_t rows;
-    pack_quads(c, lo, hi, rows);
-    const uint32_t rm = quad_rowmask(rows, q);
+    uint32_t rm;
+    pack_quads(c, q, lo, hi, rm);
     if (lb < nloc) {
       s_img[(2 * q) * kK2Group + lb] = lo;
       s_img[(2 * q + 1) * kK2Group + lb] = hi;
@@ -1097,7 +1068,7 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
   __syncthreads();
   // ---- phase 2: K2 over the LDS image (its scratch over the transpose tiles)
   TileScratch& sc = *reinterpret_cast<TileScratch*>(&s_tile[0][0]);
-  const LdsCoef src{s_img, s_rmk, coef, nzm, f * G.cum[3] + g0};
+  const LdsCoef src{s_img, s_rmk, coef, rmask, f * G.cum[3] + g0};
   encode_tile(src, sc, T, nloc, stage, tinfo, sizes, srcoff, work, work_count);
 }
 
@@ -1106,7 +1077,7 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
 // *work_count), 64 per workgroup; the grid is sized for the worst case, idle
 // groups exit.  Lists of at most `limit` blocks go to k_huff_encode_wave instead.
 __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __restrict__ coef,
-                                                        const uint2* __restrict__ nzm,
+                                                        const uint8_t* __restrict__ rmask,
                                                         const uint4* __restrict__ zq, FrameGeom G,
                                                         uint32_t* __restrict__ oslots,
                                                         uint8_t* __restrict__ sizes,
@@ -1125,7 +1096,7 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
     const bool live = i < cnt;
     const uint32_t g = live ? work[i] : 0;
     CoefRegs R;
-    R.load(coef, zq, g, live ? rowmask_of(nzm[g]) : 0u);
+    R.load(coef, zq, g, live ? rmask[g] : 0u);
     const int msz = live ? R.msz() : 0;
     const int wmsz = wave_max<kWideLanes>(msz);
     if (live) {

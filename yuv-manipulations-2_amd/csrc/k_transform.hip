@@ -88,7 +88,7 @@ using namespace xf;
 // DCT.cpp:297-306 (gather, x - 128), :269-277 (applyDCTBlock).
 __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t* __restrict__ frame, FrameGeom G,
                                                    const QTables* __restrict__ qt,
-                                                   uint4* __restrict__ coef, uint16_t* __restrict__ nzm,
+                                                   uint4* __restrict__ coef, uint8_t* __restrict__ rmask,
                                                    uint4* __restrict__ sink, uint32_t* __restrict__ k2ctl) {
 #if MYYUV_K1_PRIO > 0
   // wave issue priority over the other launch groups' kernels on the SIMD
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
   // prefetch: the loop top then waits with vmcnt(2) on every path
   sink[lane] = make_uint4(0, 0, 0, 0);
   sink[64 + lane] = make_uint4(0, 0, 0, 0);
-  reinterpret_cast<uint16_t*>(sink + 128)[lane] = 0;
+  reinterpret_cast<uint8_t*>(sink + 128)[lane] = 0;
 
   for (; ua < nall; ua += stride) {
     const uint32_t f = div_magic(ua, G.umag);
@@ -156,26 +156,21 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
     // ---- store rows 2q, 2q+1 = coefficient quads 2q, 2q+1 of the block
     {
       uint4 lo, hi;
-      uint32_t rows;
-      pack_quads(c, lo, hi, rows);
+      uint32_t rm;
+      pack_quads(c, q, lo, hi, rm);
 #if MYYUV_EXP == 2
-      if ((lo.x ^ hi.y ^ lo.z ^ hi.w ^ rows) == 0x7f3e5a11u) {  // never (keeps the transform live)
+      if ((lo.x ^ hi.y ^ lo.z ^ hi.w ^ rm) == 0x7f3e5a11u) {  // never (keeps the transform live)
         *dlo = lo;
         *dhi = hi;
       }
 #else
-      // The block's nonzero map (8 B, byte r = row r; this lane writes rows
-      // 2q, 2q+1): K2 classifies the blocks of a tile from it, and an
-      // all-zero row is not stored (the readers take a masked-off row from a
-      // zero buffer), which saves most of the 128 B per block of a q=50 frame
-      // twice (this write, K2's read).  Every lane still issues its three
-      // stores (the sink takes the skipped ones).
-      const bool nzl = (rows & 0xFFu) != 0u, nzh = (rows >> 8) != 0u;
-#ifdef MYYUV_NZM_SINK  // diagnostic build: the map to the sink (invalid output; K1 timing only)
-      *(reinterpret_cast<uint16_t*>(sink + 128) + lane) = (uint16_t)rows;
-#else
-      *(live ? nzm + (size_t)g * 4 + q : reinterpret_cast<uint16_t*>(sink + 128) + lane) = (uint16_t)rows;
-#endif
+      // Row mask for K2 (bit c: row c has a nonzero coefficient), from the
+      // block's four lanes; an all-zero row is not stored (K2 reads masked-off
+      // rows from a zero buffer), which saves most of the 128 B per block of
+      // a q=50 frame twice (this write, K2's read).  Every lane still issues
+      // its three stores (the sink takes the skipped ones).
+      const bool nzl = (rm >> (2 * q)) & 1u, nzh = (rm >> (2 * q + 1)) & 1u;
+      *(live ? rmask + g : reinterpret_cast<uint8_t*>(sink + 128) + lane) = (uint8_t)rm;
       *(nzl ? dlo : sink + lane) = lo;
       *(nzh ? dhi : sink + 64 + lane) = hi;
 #endif

@@ -23,19 +23,19 @@
 #include "myyuv_hip.h"
 
 namespace myyuv_gpu {
-__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint16_t*, uint4*, uint32_t*);
+__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*);
 __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*,
                                uint4*);
 __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*, const uint32_t*,
                               const uint32_t*, FrameGeom, uint32_t, uint32_t, const QTables*, uint4*, uint8_t*,
                               unsigned long long*);
-__global__ void k_huff_encode(const uint4*, const uint16_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
+__global__ void k_huff_encode(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
                               uint8_t*, uint16_t*, uint32_t*, uint32_t*);
-__global__ void k_huff_encode_wave(const uint4*, const uint2*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
+__global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
                                    const uint32_t*, const uint32_t*, uint32_t);
-__global__ void k_huff_encode_wide(const uint4*, const uint2*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
+__global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
                                    uint32_t*, const uint32_t*, const uint32_t*, uint32_t);
-__global__ void k_encode_tile(const uint8_t*, FrameGeom, const QTables*, uint4*, uint2*, uint32_t*, uint32_t*,
+__global__ void k_encode_tile(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint32_t*, uint32_t*,
                               uint8_t*, uint16_t*, uint32_t*, uint32_t*);
 __global__ void k_tile_scan(uint32_t*, FrameGeom, uint8_t*, uint32_t, uint32_t*, unsigned long long*);
 __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
@@ -177,8 +177,6 @@ struct myyuv_hip_ctx {
   DevBuf bmp;   // staged BMP pixels (host-buffer BMP -> IYUV)
   DevBuf bsizes;  // u32 payload sizes of a host-buffer batch
   DevBuf rmask; // per block: bit c = coefficient row c nonzero (K5 -> K6)
-  DevBuf nzm;   // per block: K1's 8-byte nonzero map, byte r = row r, bit c = column c (K1 -> K2 and the
-                // overflow passes: classification and the rows stored)
   DevBuf zq;    // 256 zero bytes: K6's source for rows the mask says are zero
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
@@ -324,7 +322,6 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->srcoff.grow((size_t)nblk * 2);
   e |= c->sizes.grow((size_t)nwaves * kWave);
   e |= c->rmask.grow((size_t)nblk);
-  e |= c->nzm.grow((size_t)nblk * 8);
   if (c->zq.n == 0) {
     e |= c->zq.grow(256);
     if (!e && hipMemset(c->zq.p, 0, 256) != hipSuccess) e |= MYYUV_E_HIP;
@@ -332,7 +329,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->loff.grow((size_t)nblk * 4);
   e |= c->tiles.grow((size_t)nf * (ntiles + 1) * 4);
   e |= c->err.grow(8);
-  e |= c->sink.grow(192 * 16);  // K1/K6: 2 x 64 quads, then K1's 64 x 2 map bytes (quad 128)
+  e |= c->sink.grow(192 * 16);  // K1/K6: 2 x 64 quads + K1's 64 mask bytes
   e |= c->psize.grow(4);
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
   e |= c->work.grow((size_t)nblk * 4 + 256);  // [0]: overflow count, then block ids
@@ -367,7 +364,8 @@ int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   uint32_t* list = count + 64;
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
   const int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(G.tcum[3], nf), dim3(kK2Group), s,
-               c->coef.as<const uint4>(), c->nzm.as<const uint16_t>(), c->zq.as<const uint4>(), G, c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
+               c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
+               c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
                c->srcoff.as<uint16_t>(), list, count);
   return e | launch_overflow(c, G, s);
 }
@@ -380,12 +378,12 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   int e = 0;
   if (limit > 0)
     e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
-                c->coef.as<const uint4>(), c->nzm.as<const uint2>(), G, c->oslots.as<uint32_t>(),
+                c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), G, c->oslots.as<uint32_t>(),
                 c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
                 limit);
   const uint32_t wide = ceil_div(nblk, kWideLanes) < kWideGrid ? ceil_div(nblk, kWideLanes) : kWideGrid;
   e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(wide), dim3(kWideLanes), s,
-              c->coef.as<const uint4>(), c->nzm.as<const uint2>(), c->zq.as<const uint4>(), G,
+              c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
               c->oslots.as<uint32_t>(), c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list,
               (const uint32_t*)count, limit);
   return e;
@@ -404,13 +402,13 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
     uint32_t* count = c->work.as<uint32_t>();
     e |= hipMemsetAsync(count, 0, 4, s) != hipSuccess;
     e |= launch(c, MYYUV_K_ENCODE_TILE, k_encode_tile, dim3(G.tcum[3], nf), dim3(kK2Group), s,
-                static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->nzm.as<uint2>(),
+                static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
                 c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(), c->srcoff.as<uint16_t>(),
                 count + 64, count);
     e |= launch_overflow(c, G, s);
   } else {
     e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
-                static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->nzm.as<uint16_t>(),
+                static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
                 c->sink.as<uint4>(), c->work.as<uint32_t>());
     if ((c->skip >> MYYUV_K_FDCT) & 1u)  // diagnostic skip: keep K1's reset of the overflow count
       e |= hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess;
@@ -651,7 +649,7 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
     if (e) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->stage, &c->oslots, &c->tinfo, &c->srcoff, &c->sizes, &c->loff, &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
-                    &c->bmp,   &c->rmask, &c->nzm, &c->zq, &c->bsizes};
+                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1065,20 +1063,19 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
     return MYYUV_E_HIP;
   hipLaunchKernelGGL(k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), 0, s,
                      c->frame.as<const uint8_t>(), G, c->qtd.as<const QTables>(), c->coef.as<uint4>(),
-                     c->nzm.as<uint16_t>(), c->sink.as<uint4>(), (uint32_t*)nullptr);
+                     c->rmask.as<uint8_t>(), c->sink.as<uint4>(), (uint32_t*)nullptr);
   std::vector<uint32_t> words((size_t)ceil_div(nblocks, kWave) * kCoefQuadsPerWave * 4);
-  std::vector<uint2> maps(nblocks);
+  std::vector<uint8_t> rm(nblocks);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(words.data(), c->coef.p, words.size() * 4, hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
-      hipMemcpyAsync(maps.data(), c->nzm.p, (size_t)nblocks * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(rm.data(), c->rmask.p, nblocks, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return MYYUV_E_HIP;
   for (uint32_t g = 0; g < nblocks; g++) {
     int16_t nat[64];
-    const uint32_t rm = rowmask_of(maps[g]);
-    for (uint32_t c4 = 0; c4 < 8; c4++) {  // rows K1 left out of the image (map byte zero) are zero
-      if ((rm >> c4) & 1u)
+    for (uint32_t c4 = 0; c4 < 8; c4++) {  // rows K1 left out of the image (mask bit clear) are zero
+      if ((rm[g] >> c4) & 1u)
         std::memcpy(nat + 8 * c4, &words[(size_t)coef_quad(g, c4) * 4], 16);
       else
         std::memset(nat + 8 * c4, 0, 16);
@@ -1108,17 +1105,14 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   const uint32_t nwaves = ceil_div(nblocks, kWave);
   // host-side relayout into K1's output format: natural-order quads
   std::vector<uint32_t> words((size_t)nwaves * kCoefQuadsPerWave * 4, 0u);
-  std::vector<uint64_t> maps(nblocks, 0u);  // K1's nonzero maps (byte r = row r, bit c = column c)
   for (uint32_t g = 0; g < nblocks; g++) {
     int16_t nat[64];
     for (int z = 0; z < 64; z++) nat[kZigzag[z]] = coef_zz[(size_t)g * 64 + z];
     for (uint32_t c4 = 0; c4 < 8; c4++)
       std::memcpy(&words[(size_t)coef_quad(g, c4) * 4], nat + 8 * c4, 16);
-    for (int n = 0; n < 64; n++)
-      if (nat[n] != 0) maps[g] |= 1ull << n;
   }
   if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->nzm.p, maps.data(), (size_t)nblocks * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemsetAsync(c->rmask.p, 0xFF, nblocks, s) != hipSuccess ||  // every row present
       hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess)  // K1 zeroes it in the codec path
     return MYYUV_E_HIP;
   if (launch_huff_encode(c, G, s)) return MYYUV_E_HIP;

@@ -253,37 +253,8 @@ __device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_
 // Rows 2q, 2q+1 of the block as two coefficient quads (codec_common.hpp
 // layout) and the block's row mask (bit c: row c has a nonzero coefficient),
 // from its four lanes (lanes 4b .. 4b+3 of the wave).
-// v_pk_min_u16 (w, 0x00010001): each 16-bit half of w clamped to 0 / 1
-__device__ __forceinline__ uint32_t pk_nz16(uint32_t w, uint32_t ones) {
-  uint32_t r;
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(w), "v"(ones));
-  return r;
-}
-
-// Nonzero pattern of one coefficient row held as a quad (word k = columns 2k,
-// 2k+1): bit c = column c is nonzero.
-__device__ __forceinline__ uint32_t row_bits(const uint4& v) {
-#if defined(MYYUV_ROWBITS_SWAR)  // tuning build: the flags by 32-bit SWAR instead of v_pk_min_u16
-  uint32_t u = 0;
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int k = 0; k < 4; k++) u |= ((((w[k] & 0x7FFF7FFFu) + 0x7FFF7FFFu) | w[k]) & 0x80008000u) >> (15 - 2 * k);
-  return (u | (u >> 15)) & 0xFFu;
-#else
-  const uint32_t ones = 0x00010001u;
-  const uint32_t u = pk_nz16(v.x, ones) | (pk_nz16(v.y, ones) << 2) | (pk_nz16(v.z, ones) << 4) |
-                     (pk_nz16(v.w, ones) << 6);
-  return (u | (u >> 15)) & 0xFFu;  // columns 2k + 1 (bits 16 + 2k) down to bit 2k + 1
-#endif
-}
-
-// Packs lane (b, q)'s 16 quantised outputs into its two coefficient quads
-// (rows 2q, 2q+1) and gives the lane's two rows' nonzero patterns `rows`
-// (byte 0: row 2q, byte 1: row 2q+1, bit c = column c): the block's 8-byte
-// nonzero map (byte r = row r) is the four lanes' `rows`, from which K2
-// classifies blocks without loading their coefficients and the coefficient
-// readers know which rows were stored.
-__device__ __forceinline__ void pack_quads(const uint32_t (&c)[16], uint4& lo, uint4& hi, uint32_t& rows) {
+__device__ __forceinline__ void pack_quads(const uint32_t (&c)[16], uint32_t q, uint4& lo, uint4& hi,
+                                           uint32_t& rm) {
   lo.x = __builtin_amdgcn_perm(c[2], c[0], 0x05040100u);
   lo.y = __builtin_amdgcn_perm(c[6], c[4], 0x05040100u);
   lo.z = __builtin_amdgcn_perm(c[10], c[8], 0x05040100u);
@@ -292,15 +263,10 @@ __device__ __forceinline__ void pack_quads(const uint32_t (&c)[16], uint4& lo, u
   hi.y = __builtin_amdgcn_perm(c[7], c[5], 0x05040100u);
   hi.z = __builtin_amdgcn_perm(c[11], c[9], 0x05040100u);
   hi.w = __builtin_amdgcn_perm(c[15], c[13], 0x05040100u);
-  rows = row_bits(lo) | (row_bits(hi) << 8);
-}
-
-// The block's row mask (bit c: row c nonzero) from its four lanes' `rows`.
-__device__ __forceinline__ uint32_t quad_rowmask(uint32_t rows, uint32_t q) {
-  uint32_t rm = ((rows & 0xFFu) != 0u ? 1u << (2 * q) : 0u) | ((rows >> 8) != 0u ? 2u << (2 * q) : 0u);
+  const bool nzl = (lo.x | lo.y | lo.z | lo.w) != 0u, nzh = (hi.x | hi.y | hi.z | hi.w) != 0u;
+  rm = (nzl ? 1u << (2 * q) : 0u) | (nzh ? 2u << (2 * q) : 0u);
   rm |= __shfl_xor(rm, 1, 64);
   rm |= __shfl_xor(rm, 2, 64);
-  return rm;
 }
 
 // K6's body for lane (b, q) of a 16-block unit (DCT.cpp:325-335, :358-362):
