@@ -103,16 +103,17 @@ constexpr float kNearRel = 0x1p-21f;
 // coefficients are consumed (K2) or produced (K5).
 constexpr uint32_t kCoefQuadsPerWave = 8 * 64;
 
-// Worklists of blocks with more than 16 distinct symbols (what the CAP-16
-// tier k_huff_encode_r16 leaves) up to this many blocks are encoded
-// wave-per-block (k_huff_encode_wave), longer ones lane-per-block with the
-// CAP-64 LDS replay (k_huff_encode_wide).
+// K2 overflow worklists up to this many blocks are encoded wave-per-block
+// (k_huff_encode_wave), longer ones lane-per-block (k_huff_encode_wide).
 #ifndef MYYUV_WAVE_LIMIT
 #define MYYUV_WAVE_LIMIT 24576
 #endif
 constexpr uint32_t kWaveEncodeLimit = MYYUV_WAVE_LIMIT;
+#ifndef MYYUV_BATCH_WAVE_LIMIT
+#define MYYUV_BATCH_WAVE_LIMIT 0
+#endif
+constexpr uint32_t kBatchWaveLimit = MYYUV_BATCH_WAVE_LIMIT;  // the same limit for batches (nframes > 1)
 constexpr uint32_t kWaveEncodeGrid = 8192;   // waves of k_huff_encode_wave (grid-stride)
-constexpr uint32_t kR16Grid = 4096;          // workgroups of k_huff_encode_r16 (grid-stride, 64 blocks each)
 #ifndef MYYUV_WIDE_LANES
 #define MYYUV_WIDE_LANES 64
 #endif

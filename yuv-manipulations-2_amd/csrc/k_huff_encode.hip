@@ -60,7 +60,6 @@ extern __device__ uint32_t g_k2_fstamps[8192 * 8];
   } while (0)
 #endif
 #include "huff_common.hpp"
-#include "huff_r16.hpp"
 #include "xform_common.hpp"
 
 namespace myyuv_gpu {
@@ -1104,54 +1103,6 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
       const Img<CAP> I{lds, (int)threadIdx.x};
       encode_block<CAP>(I, R, msz, max(wmsz, 1), oslots + (size_t)g * kSlotWords, sizes + g);
       atomicAdd(tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, (uint32_t)sizes[g]);  // (this lane's own store)
-    }
-  }
-}
-
-// Overflow tier 1 (register-resident, CAP 16; huff_r16.hpp), lane per block:
-// the blocks K2 listed in `work` (more than 8 distinct symbols), 64 per
-// workgroup, grid-stride; blocks with more than 16 go on to `work2` for the
-// wave-per-block / CAP-64 passes.  Natural images put nearly all overflow
-// blocks here (q50: 99.8 %), so the pass's time is one lane's register
-// program instead of the CAP-64 LDS replay's chain of dependent LDS round
-// trips.
-__global__ __launch_bounds__(64) void k_huff_encode_r16(const uint4* __restrict__ coef,
-                                                        const uint8_t* __restrict__ rmask,
-                                                        const uint4* __restrict__ zq, FrameGeom G,
-                                                        uint32_t* __restrict__ oslots,
-                                                        uint8_t* __restrict__ sizes,
-                                                        uint32_t* __restrict__ tinfo,
-                                                        const uint32_t* __restrict__ work,
-                                                        const uint32_t* __restrict__ work_count,
-                                                        uint32_t* __restrict__ work2,
-                                                        uint32_t* __restrict__ work2_count) {
-  const uint32_t cnt = *work_count;
-  const uint32_t lane = threadIdx.x;
-  for (uint32_t base = blockIdx.x * kWave; base < cnt; base += gridDim.x * kWave) {
-    const uint32_t i = base + lane;
-    const bool live = i < cnt;
-    const uint32_t g = live ? work[i] : 0u;
-    CoefRegs R;
-    R.load(coef, zq, g, live ? rmask[g] : 0u);
-    const int msz = live ? R.msz() : 0;
-    const int wmsz = max(wave_max(msz), 1);
-    EncState16 S;
-    const bool ok = live && build_r16(R, msz, wmsz, S);
-    if (ok) {
-      BitWriter bw;
-      bw.out = oslots + (size_t)g * kSlotWords;
-      emit_chunk16(S, wmsz, bw);
-      bw.align_byte();
-      bw.flush();
-      sizes[g] = (uint8_t)S.size;
-      atomicAdd(tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, S.size);  // the tile's overflow bytes
-    }
-    const uint64_t more = __ballot(live && !ok);
-    if (more) {
-      uint32_t b0 = 0;
-      if (lane == 0) b0 = atomicAdd(work2_count, (uint32_t)__popcll(more));
-      b0 = __builtin_amdgcn_readfirstlane(b0);
-      if ((more >> lane) & 1ull) work2[b0 + (uint32_t)__popcll(more & ((1ull << lane) - 1ull))] = g;
     }
   }
 }

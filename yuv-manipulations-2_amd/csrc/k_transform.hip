@@ -94,8 +94,8 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
   // wave issue priority over the other launch groups' kernels on the SIMD
   __builtin_amdgcn_s_setprio(MYYUV_K1_PRIO);
 #endif
-  // K2's overflow counts for the launch that follows in the stream (nullptr: none)
-  if (k2ctl != nullptr && blockIdx.x == 0 && threadIdx.x < 2) k2ctl[threadIdx.x] = 0u;
+  // K2's overflow count for the launch that follows in the stream (nullptr: none)
+  if (k2ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *k2ctl = 0u;
   __shared__ float tile[4][kXfUnit * kTile];
   __shared__ float sqr[2 * 3 * 64];  // QTables::q then QTables::r
   static_assert(offsetof(QTables, r) == sizeof(float) * 3 * 64, "layout");

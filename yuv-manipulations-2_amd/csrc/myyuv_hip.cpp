@@ -35,8 +35,6 @@ __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint
                                    const uint32_t*, const uint32_t*, uint32_t);
 __global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
                                    uint32_t*, const uint32_t*, const uint32_t*, uint32_t);
-__global__ void k_huff_encode_r16(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
-                                  uint32_t*, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_encode_tile(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint32_t*, uint32_t*,
                               uint8_t*, uint16_t*, uint32_t*, uint32_t*);
 __global__ void k_tile_scan(uint32_t*, FrameGeom, uint8_t*, uint32_t, uint32_t*, unsigned long long*);
@@ -205,6 +203,11 @@ struct myyuv_hip_ctx {
   int64_t launches[MYYUV_K_COUNT] = {};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> free_events;
+  // host-buffer entry points: two pinned chunks, so the CPU copy of one chunk
+  // runs while the DMA engine moves the other (pageable copies go through the
+  // runtime's own staging at a fraction of the link rate)
+  uint8_t* pin = nullptr;
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
   std::mutex mu;
 };
 
@@ -329,7 +332,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->sink.grow(192 * 16);  // K1/K6: 2 x 64 quads + K1's 64 mask bytes
   e |= c->psize.grow(4);
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
-  e |= c->work.grow((size_t)nblk * 8 + 256);  // [0], [1]: overflow counts, then the two lists
+  e |= c->work.grow((size_t)nblk * 4 + 256);  // [0]: overflow count, then block ids
   const size_t st_bytes = (size_t)nf * (ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
@@ -346,24 +349,21 @@ uint32_t next_epoch(myyuv_hip_ctx* c) {
   return c->epoch;
 }
 
-// K2: the CAP-8 pass over all tiles (grid (tiles, frames)), then the
-// overflow tiers over the blocks it listed (more than 8 distinct symbols;
-// worklists filled on the device, no host sync):
-//   1. k_huff_encode_r16: register-resident, up to 16 symbols (nearly every
-//      overflow block of a natural image); it lists the rest in work2;
-//   2. work2: wave per block (k_huff_encode_wave) when it is at most
-//      kWaveEncodeLimit blocks long, else lane per block with the CAP-64 LDS
-//      replay (k_huff_encode_wide, noise-like frames).
-// Every kernel is queued; each returns at once outside its regime.
-// work: [0] K2's count, [1] work2's count (both zeroed by K1 or the host),
-// K2's list from word 64, work2 from word 64 + nblk.
+// K2: fast pass over all tiles (grid (tiles, frames)), then the overflow pass
+// over the blocks with more than 8 distinct symbols (worklist filled on the
+// device; no host sync): wave-per-block for lists of at most kWaveEncodeLimit
+// blocks, lane-per-block for longer ones; both kernels are queued and each
+// returns at once outside its regime.  A batch (nf > 1) takes the
+// lane-per-block pass only: its list is long, and the wave pass's per-block
+// SALU cost would crowd the other launch groups in flight (tools/kskip.py).
 int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s);
 
 int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
+  const uint32_t nf = G.nframes;
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
-  const int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(G.tcum[3], G.nframes), dim3(kK2Group), s,
+  const int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(G.tcum[3], nf), dim3(kK2Group), s,
                c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
                c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
                c->srcoff.as<uint16_t>(), list, count);
@@ -371,25 +371,21 @@ int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
 }
 
 int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
-  const uint32_t nblk = G.cum[3] * G.nframes;
+  const uint32_t nf = G.nframes, nblk = G.cum[3] * nf;
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
-  uint32_t* count2 = count + 1;
-  uint32_t* list2 = list + nblk;
-  const uint32_t r16 = ceil_div(nblk, kWave) < kR16Grid ? ceil_div(nblk, kWave) : kR16Grid;
-  int e = launch(c, MYYUV_K_HUFF_R16, k_huff_encode_r16, dim3(r16), dim3(kWave), s, c->coef.as<const uint4>(),
-                 c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G, c->oslots.as<uint32_t>(),
-                 c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
-                 list2, count2);
-  e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
-              c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), G, c->oslots.as<uint32_t>(),
-              c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list2, (const uint32_t*)count2,
-              kWaveEncodeLimit);
+  const uint32_t limit = nf > 1 ? kBatchWaveLimit : kWaveEncodeLimit;
+  int e = 0;
+  if (limit > 0)
+    e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
+                c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), G, c->oslots.as<uint32_t>(),
+                c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
+                limit);
   const uint32_t wide = ceil_div(nblk, kWideLanes) < kWideGrid ? ceil_div(nblk, kWideLanes) : kWideGrid;
   e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(wide), dim3(kWideLanes), s,
               c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
-              c->oslots.as<uint32_t>(), c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list2,
-              (const uint32_t*)count2, kWaveEncodeLimit);
+              c->oslots.as<uint32_t>(), c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list,
+              (const uint32_t*)count, limit);
   return e;
 }
 
@@ -404,7 +400,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   if (c->fused) {
     // fused single-pass encoder (K1 + K2 per tile), then the overflow passes
     uint32_t* count = c->work.as<uint32_t>();
-    e |= hipMemsetAsync(count, 0, 8, s) != hipSuccess;
+    e |= hipMemsetAsync(count, 0, 4, s) != hipSuccess;
     e |= launch(c, MYYUV_K_ENCODE_TILE, k_encode_tile, dim3(G.tcum[3], nf), dim3(kK2Group), s,
                 static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
                 c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(), c->srcoff.as<uint16_t>(),
@@ -415,7 +411,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
                 static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
                 c->sink.as<uint4>(), c->work.as<uint32_t>());
     if ((c->skip >> MYYUV_K_FDCT) & 1u)  // diagnostic skip: keep K1's reset of the overflow count
-      e |= hipMemsetAsync(c->work.p, 0, 8, s) != hipSuccess;
+      e |= hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess;
     e |= launch_huff_encode(c, G, s);
   }
   e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(256), s, c->tinfo.as<uint32_t>(), G,
@@ -463,17 +459,44 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
   return e ? MYYUV_E_HIP : 0;
 }
 
-// Host <-> device copies of the host-buffer entry points: direct async copies
-// from / into the caller's pageable buffers.  On this stack they run at the
-// PCIe link rate whatever the buffer's alignment or age (tools/ubench/
-// pcie_copy.cpp, profiles/r3b_pcie_copy.txt: 18 MB in 0.33-0.43 ms, a fresh
-// or 1-byte-misaligned buffer included), faster than staging through pinned
-// chunks with a CPU copy (0.47-0.59 ms H2D, 1.1-2.7 ms D2H).
-int h2d(myyuv_hip_ctx*, void* dst, const void* src, size_t n, hipStream_t s) {
-  return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : MYYUV_E_HIP;
+// Host-to-device copies of the host-buffer entry points, through the
+// context's two pinned chunks: chunk i is copied on the CPU into pinned
+// buffer i & 1 while the DMA of chunk i - 1 runs.  Small copies go direct.
+// (A direct copy from pageable memory measured 11.7 ms for a 4032x3008 frame,
+// the staged one 1.7 ms including the compression: tools/host_api_rate.py.)
+constexpr size_t kPinChunk = 2u << 20;
+constexpr size_t kPinMin = 4u << 20;  // (a 3.4 MB payload went faster direct: 3.41 vs 3.68 ms per decode)
+
+int pin_ready(myyuv_hip_ctx* c) {
+  if (c->pin) return 0;
+  if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), 2 * kPinChunk, hipHostMallocDefault) != hipSuccess) {
+    c->pin = nullptr;
+    return MYYUV_E_HIP;
+  }
+  for (auto& e : c->pin_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return MYYUV_E_HIP;
+  return 0;
 }
 
-// (synchronous: returns when dst holds the bytes)
+int h2d(myyuv_hip_ctx* c, void* dst, const void* src, size_t n, hipStream_t s) {
+  if (n < kPinMin || pin_ready(c))
+    return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : MYYUV_E_HIP;
+  for (size_t off = 0, i = 0; off < n; off += kPinChunk, i++) {
+    const size_t len = std::min(kPinChunk, n - off);
+    uint8_t* buf = c->pin + (i & 1) * kPinChunk;
+    if (i >= 2 && hipEventSynchronize(c->pin_ev[i & 1]) != hipSuccess) return MYYUV_E_HIP;  // its last DMA is done
+    std::memcpy(buf, static_cast<const uint8_t*>(src) + off, len);
+    if (hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, buf, len, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipEventRecord(c->pin_ev[i & 1], s) != hipSuccess)
+      return MYYUV_E_HIP;
+  }
+  return 0;
+}
+
+// (synchronous: returns when dst holds the bytes.  Device-to-host copies into
+// pageable memory run at the link rate on this stack (measured: 3.41 ms
+// direct against 3.87 ms through the pinned chunks for a 4032x3008 decode),
+// so they go direct.)
 int d2h(myyuv_hip_ctx*, void* dst, const void* src, size_t n, hipStream_t s) {
   return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess
              ? 0
@@ -621,6 +644,9 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->done);
+  if (c->pin) (void)hipHostFree(c->pin);
+  for (auto e : c->pin_ev)
+    if (e) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->stage, &c->oslots, &c->tinfo, &c->srcoff, &c->sizes, &c->loff, &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
                     &c->bmp,   &c->rmask, &c->zq, &c->bsizes};
@@ -1087,7 +1113,7 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   }
   if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemsetAsync(c->rmask.p, 0xFF, nblocks, s) != hipSuccess ||  // every row present
-      hipMemsetAsync(c->work.p, 0, 8, s) != hipSuccess)  // K1 zeroes them in the codec path
+      hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess)  // K1 zeroes it in the codec path
     return MYYUV_E_HIP;
   if (launch_huff_encode(c, G, s)) return MYYUV_E_HIP;
   // K2's hand-off (codec_common.hpp): per tile the waves' dense runs, the
