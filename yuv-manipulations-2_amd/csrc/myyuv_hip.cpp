@@ -203,11 +203,6 @@ struct myyuv_hip_ctx {
   int64_t launches[MYYUV_K_COUNT] = {};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> free_events;
-  // host-buffer entry points: two pinned chunks, so the CPU copy of one chunk
-  // runs while the DMA engine moves the other (pageable copies go through the
-  // runtime's own staging at a fraction of the link rate)
-  uint8_t* pin = nullptr;
-  hipEvent_t pin_ev[2] = {nullptr, nullptr};
   std::mutex mu;
 };
 
@@ -459,44 +454,17 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
   return e ? MYYUV_E_HIP : 0;
 }
 
-// Host-to-device copies of the host-buffer entry points, through the
-// context's two pinned chunks: chunk i is copied on the CPU into pinned
-// buffer i & 1 while the DMA of chunk i - 1 runs.  Small copies go direct.
-// (A direct copy from pageable memory measured 11.7 ms for a 4032x3008 frame,
-// the staged one 1.7 ms including the compression: tools/host_api_rate.py.)
-constexpr size_t kPinChunk = 2u << 20;
-constexpr size_t kPinMin = 4u << 20;  // (a 3.4 MB payload went faster direct: 3.41 vs 3.68 ms per decode)
-
-int pin_ready(myyuv_hip_ctx* c) {
-  if (c->pin) return 0;
-  if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), 2 * kPinChunk, hipHostMallocDefault) != hipSuccess) {
-    c->pin = nullptr;
-    return MYYUV_E_HIP;
-  }
-  for (auto& e : c->pin_ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return MYYUV_E_HIP;
-  return 0;
+// Host <-> device copies of the host-buffer entry points: direct async copies
+// from / into the caller's pageable buffers.  On this stack they run at the
+// PCIe link rate whatever the buffer's alignment or age (tools/ubench/
+// pcie_copy.cpp, profiles/r3b_pcie_copy.txt: 18 MB in 0.33-0.43 ms, a fresh
+// or 1-byte-misaligned buffer included), faster than staging through pinned
+// chunks with a CPU copy (0.47-0.59 ms H2D, 1.1-2.7 ms D2H).
+int h2d(myyuv_hip_ctx*, void* dst, const void* src, size_t n, hipStream_t s) {
+  return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : MYYUV_E_HIP;
 }
 
-int h2d(myyuv_hip_ctx* c, void* dst, const void* src, size_t n, hipStream_t s) {
-  if (n < kPinMin || pin_ready(c))
-    return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : MYYUV_E_HIP;
-  for (size_t off = 0, i = 0; off < n; off += kPinChunk, i++) {
-    const size_t len = std::min(kPinChunk, n - off);
-    uint8_t* buf = c->pin + (i & 1) * kPinChunk;
-    if (i >= 2 && hipEventSynchronize(c->pin_ev[i & 1]) != hipSuccess) return MYYUV_E_HIP;  // its last DMA is done
-    std::memcpy(buf, static_cast<const uint8_t*>(src) + off, len);
-    if (hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, buf, len, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipEventRecord(c->pin_ev[i & 1], s) != hipSuccess)
-      return MYYUV_E_HIP;
-  }
-  return 0;
-}
-
-// (synchronous: returns when dst holds the bytes.  Device-to-host copies into
-// pageable memory run at the link rate on this stack (measured: 3.41 ms
-// direct against 3.87 ms through the pinned chunks for a 4032x3008 decode),
-// so they go direct.)
+// (synchronous: returns when dst holds the bytes)
 int d2h(myyuv_hip_ctx*, void* dst, const void* src, size_t n, hipStream_t s) {
   return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess
              ? 0
@@ -644,9 +612,6 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   drain_profile(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->done);
-  if (c->pin) (void)hipHostFree(c->pin);
-  for (auto e : c->pin_ev)
-    if (e) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->stage, &c->oslots, &c->tinfo, &c->srcoff, &c->sizes, &c->loff, &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
                     &c->bmp,   &c->rmask, &c->zq, &c->bsizes};
