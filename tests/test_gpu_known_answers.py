@@ -187,3 +187,17 @@ def test_batch4k_512_frames_gathered(codec, oracle, chef_big):
         want = np.frombuffer(oracle.decompress(pays[i], w, h, q), np.uint8)
         for a, b in ((0, w * h), (w * h, w * h * 5 // 4), (w * h * 5 // 4, fb)):  # Y, U, V
             assert np.abs(gd[a:b].astype(int) - want[a:b].astype(int)).max() == 0, i
+
+
+def test_repeated_compress_stable(codec, tiled8k):
+    """Back-to-back compressions of one frame on one context reuse every
+    workspace buffer (stage, overflow slots, tile info): each must reproduce
+    the known answer.  (A cross-lane change that passed the single-shot tests
+    once broke this in a few chunks per frame: profiles/r3h_dpp_bisect.txt.)"""
+    pays = [codec.compress(tiled8k, 8192, 8192, (90, 90, 90)) for _ in range(6)]
+    assert [len(p) for p in pays] == [19242133] * 6
+    assert len({sha(p) for p in pays}) == 1
+    import myyuv_file
+    img = myyuv_file.YUVFile(width=8192, height=8192, data=tiled8k)
+    assert sha(img.compressed(bytes([90] * 3), pays[0]).dumps()) == \
+        "6f0fcfaeeae152f764ed46c8c8973345cfffbe54e2e3850a8bf7ca792e85fc05"

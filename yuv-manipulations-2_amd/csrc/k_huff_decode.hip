@@ -46,9 +46,15 @@ namespace {
 constexpr uint32_t kStageQuads = 384;
 
 // diagnostic ablations (never the product): 1 = no symbol decode, 2 = no
-// table parse either
+// table parse either, 3 = the fused decoder skips its transform
 #ifndef MYYUV_K5_EXP
 #define MYYUV_K5_EXP 0
+#endif
+#ifndef MYYUV_K5_GROUP
+#define MYYUV_K5_GROUP 2  // positions per "any lane left" test (1 / 2 / 4 / 8: 132.4 / 128.2 / 129.0 / 135.1 us per launch, tools/runs/r3n.sh)
+#endif
+#ifndef MYYUV_K5S_WAVES
+#define MYYUV_K5S_WAVES 5  // the split decoder's K5
 #endif
 #ifndef MYYUV_K5_WAVES
 #define MYYUV_K5_WAVES 5
@@ -147,70 +153,70 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T)
   return 0;
 }
 
-// Value of scan position j into the natural-order words (unpack11bit: 11-bit
-// two's complement, Huffman.cpp:54-69; de-zig-zag, :148-153).
-__device__ __forceinline__ void put_value(uint32_t (&nw)[32], int j, uint32_t raw, bool take) {
-  const uint32_t v = take ? (uint32_t)(((int32_t)(raw << 21)) >> 21) : 0u;
-  const int z = c_zz[j];
-  if (z & 1) nw[z >> 1] |= v << 16;
-  else nw[z >> 1] |= v & 0xFFFFu;
-}
-
 // Symbols of REGULAR tables (Huffman.cpp:106-154) into nw (natural-order
-// int16 pairs, zeroed by the caller).  Returns 0 or the MYYUV_E_* code (10
-// bad code, 11 unknown symbol) for lanes with `act`.
+// int16 pairs, zeroed by the caller).  Returns true for an `act` lane whose
+// message fails (no code matches, or a code runs past nbits): the caller
+// re-decodes that block with decode_general, which gives the reference's
+// exact outcome (10 bad code / 11 unknown symbol) — regular tables decode
+// identically on both paths, so only the error code is taken from it.
 //
 // Fully unrolled over the 64 scan positions (each value lands in a statically
-// indexed register) in groups of 8 with one uniform "any lane left" test per
-// group; inside a group the body is straight-line (state updates by select:
-// divergent branches, or an exit per position, make the compiler shuffle the
-// whole nw[] array at every join).  The 64-bit window is rebuilt every 7
-// positions (at most 56 bits consumed) from three stage words.
-// (Prefetching those words a few positions ahead, or deferring each value
+// indexed register), with a uniform "any lane left" exit before every
+// position; the body is straight-line (state updates by select: divergent
+// branches make the compiler shuffle the whole nw[] array at every join).
+// A lane's state after it stops (bp, window) is dead, so it advances
+// unconditionally; only the value store is predicated.  The 64-bit window is
+// rebuilt every 7 positions (at most 56 bits consumed) from three stage
+// words.  Per position: the length by SWAR compares, the value's 11 bits read
+// in place from the table (group bit + 11 * rank), one predicated OR.
+// (Prefetching the stage words a few positions ahead, or deferring each value
 // read by one position, measured no faster on MI355X, and with the loads
 // three positions ahead the decoded values came out wrong nondeterministically
 // in long straight-line groups: both are deliberately not done.)
-__device__ __forceinline__ int decode_regular(const LdsChunk& c, const Table& T, bool act,
-                                              uint32_t (&nw)[32]) {
-  int code = 0;
-  uint32_t bp = 0, o = 0;
-  uint64_t rwin = 0;  // MSB-first window: chunk bit sbit + bp - o at bit 63
+__device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T, bool act,
+                                               uint32_t (&nw)[32]) {
+  bool bad = false;
+  uint32_t bp = 0;
+  uint64_t rwin = 0;  // MSB-first window: the next symbol's first bit at bit 63
   act = act && T.nbits > 0;
   const uint32_t P0 = 8 * c.b0 + T.sbit;  // stage bit of the first symbol bit
+  const uint32_t vbase = 8 * c.b0 - 4096;  // stage bit of chunk bit 0, less the gpos bias
+  const uint64_t glo = ((uint64_t)T.gpos[1] << 32) | T.gpos[0];
+  const uint64_t ghi = ((uint64_t)T.gpos[3] << 32) | T.gpos[2];
 #pragma unroll
-  for (int j0 = 0; j0 < 64; j0 += 8) {
+  for (int j0 = 0; j0 < 64; j0 += MYYUV_K5_GROUP) {
     if (__ballot(act) == 0) continue;
 #pragma unroll
-    for (int j = j0; j < j0 + 8; j++) {
-      if (j % 7 == 0) {
-        const uint32_t P = P0 + bp, w = P >> 5;
-        const uint32_t q0 = c.st[w], q1 = c.st[w + 1], q2 = c.st[w + 2];
-        rwin = ((uint64_t)__brev(funnel(q1, q0, P)) << 32) | __brev(funnel(q2, q1, P));
-        o = 0;
-      }
-      const uint32_t w8 = (uint32_t)((rwin << o) >> 56);  // next 8 bits, MSB-first
-      // matched length - 1 = #{L : w8 >= lim[L]} (eight 16-bit fields)
-      const uint32_t t = w8 | 0x8000u, W = (t << 16) | t;
-      const uint32_t n = __popc((W - T.lim[0]) & 0x80008000u) +
-                         __popc((W - T.lim[1]) & 0x80008000u) +
-                         __popc((W - T.lim[2]) & 0x80008000u) +
-                         __popc((W - T.lim[3]) & 0x80008000u);
-      const uint32_t L = n + 1;
-      const bool nomatch = n == 8;
-      const bool fail = act && (nomatch || bp + L > T.nbits);
-      code = fail ? (nomatch && bp + 8 <= T.nbits ? 11 : 10) : code;
-      const bool take = act && !fail;
-      const uint64_t gsrc = (n & 4) ? (((uint64_t)T.gpos[3] << 32) | T.gpos[2])
-                                    : (((uint64_t)T.gpos[1] << 32) | T.gpos[0]);
-      const uint32_t G = (uint32_t)(gsrc >> (16 * (n & 3))) & 0xFFFF;
-      const uint32_t vbit = (w8 >> ((7 - n) & 7)) * 11 + G - 4096;  // group bit + 11 * rank
-      put_value(nw, j, c.bits32(take ? vbit : 0u), take);
-      bp = take ? bp + L : bp;
-      o = take ? o + L : o;
-      act = take && bp < T.nbits;
+  for (int j = j0; j < j0 + MYYUV_K5_GROUP; j++) {
+    if (j % 7 == 0) {
+      const uint32_t P = act ? P0 + bp : P0, w = P >> 5;
+      const uint32_t q0 = c.st[w], q1 = c.st[w + 1], q2 = c.st[w + 2];
+      rwin = ((uint64_t)__brev(funnel(q1, q0, P)) << 32) | __brev(funnel(q2, q1, P));
     }
+    const uint32_t w8 = (uint32_t)(rwin >> 56);  // next 8 bits, MSB-first
+    // matched length - 1 = #{L : w8 >= lim[L]} (eight 16-bit fields)
+    const uint32_t W = w8 * 0x10001u | 0x80008000u;
+    const uint32_t n = __popc((W - T.lim[0]) & 0x80008000u) + __popc((W - T.lim[1]) & 0x80008000u) +
+                       __popc((W - T.lim[2]) & 0x80008000u) + __popc((W - T.lim[3]) & 0x80008000u);
+    const uint32_t bpn = bp + n + 1;
+    const bool ok = n < 8 && bpn <= T.nbits;
+    bad = bad || (act && !ok);
+    const bool take = act && ok;
+    // the value: 16-bit field n of gpos (a 64-bit shift uses its count mod 64)
+    const uint32_t G = (uint32_t)((n < 4 ? glo : ghi) >> (n << 4)) & 0xFFFFu;
+    const uint32_t vbit = (w8 >> ((7 - n) & 7)) * 11u + G + vbase;
+    const uint32_t P = take ? vbit : 0u, w = P >> 5;
+    const uint32_t raw = funnel(c.st[w + 1], c.st[w], P);
+    const uint32_t v = take ? (uint32_t)(((int32_t)(raw << 21)) >> 21) : 0u;
+    const int z = c_zz[j];
+    if (z & 1) nw[z >> 1] |= v << 16;
+    else nw[z >> 1] |= v & 0xFFFFu;
+    rwin <<= (n + 1) & 63;
+    bp = bpn;
+    act = take && bpn < T.nbits;
   }
-  return code;
+  }
+  return bad;
 }
 
 // Symbols of any table, bit-serial conditions as the reference evaluates them
@@ -390,13 +396,15 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
     if (mine) pcode = parse_table(lc, s, T);
 #endif
     const bool go = mine && pcode == 0;
-    int dcode;
+    int dcode = 0;
 #if MYYUV_K5_EXP == 0
-    dcode = decode_regular(lc, T, go && T.regular, nw);
+    const bool failed = decode_regular(lc, T, go && T.regular, nw);
 #else
-    dcode = 0;
+    const bool failed = false;
 #endif
-    if (go && !T.regular) {
+    // tables the reference never writes, and failed messages (for the
+    // reference's exact error code): the bit-serial path
+    if (go && (!T.regular || failed)) {
       direct = true;
       dcode = decode_general(lc, T, coef, gbase + g);
     }
@@ -415,7 +423,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   return true;
 }
 
-__global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_huff_decode(const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64, MYYUV_K5S_WAVES) void k_huff_decode(const uint8_t* __restrict__ in,
                                                    const uint32_t* __restrict__ in_size,
                                                    uint32_t cap,
                                                    const StreamDesc* __restrict__ desc,
@@ -502,6 +510,15 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
       nw[4 * c + 3] = v.w;
     }
   }
+#if MYYUV_K5_EXP == 3
+  {
+    uint32_t x = 0;
+#pragma unroll
+    for (int w = 0; w < 32; w++) x += nw[w] * (2u * w + 1u);
+    if (x == 0x9E3779B9u) frame[lane] = 1;  // (keeps the decode live)
+    return;
+  }
+#endif
   // ---- K6 on the group, unit by unit
   const int p = D.p;
   xf::Unit U;
