@@ -54,9 +54,10 @@ extern "C" {
 
 typedef struct myyuv_hip_ctx* myyuv_hip_handle;
 
-/* Context: one per (host thread, device).  Owns a HIP stream, the per-call
- * workspace (grown on demand, never freed inside a call) and pinned staging
- * buffers for the host-buffer entry points.  Reentrant across contexts, as the
+/* Context: one per (host thread, device).  Owns a HIP stream and the per-call
+ * workspace (grown on demand, never freed inside a call); the host-buffer
+ * entry points copy straight from / into the caller's pageable buffers.
+ * Reentrant across contexts, as the
  * reference is (SURVEY.md §8b "Threading").  Calls through ONE context share
  * its workspace, so they run in call order even on different streams: a call
  * on a stream other than the previous call's makes its stream wait for the
@@ -113,7 +114,14 @@ int myyuv_gpu_dct_decompress_device(myyuv_hip_handle h, const void* d_payload,
  * A device-side error reports the batch-global block index
  * (f * blocks_per_frame + block) of the first failing block; a header error
  * of frame f > 0 reports f * blocks_per_frame.  Each frame's bytes are those
- * of the single-frame call. */
+ * of the single-frame call.
+ * Workspace (myyuv_hip_reserve_batch reserves it up front; the calls grow it
+ * on demand): about 460 B per 8x8 block of the batch — the encoder's stage
+ * (160 B: a tile's chunks, kMaxChunk per block) and overflow slots (160 B per
+ * block: any block may exceed 8 distinct symbols, as nearly all of a noise
+ * frame's do, so the slots cannot be sized from a typical list), plus the
+ * coefficients (128 B) and small per-block arrays.  A 7-frame 4032x3008 batch
+ * takes ~0.9 GB, a 16-frame 8192x8192 batch ~12 GB (of 288 GB). */
 int myyuv_hip_reserve_batch(myyuv_hip_handle h, uint32_t width, uint32_t height, uint32_t nframes);
 int myyuv_gpu_dct_compress_batch_device(myyuv_hip_handle h, const void* d_iyuv, uint32_t nframes,
                                         uint32_t width, uint32_t height, const uint8_t quality[3],

@@ -35,7 +35,9 @@ def main():
     dev = torch.device("cuda", 0)
     codec = myyuv_hip.Codec(0)
     cap = myyuv_hip.payload_bound(w, h)
-    sp = torch.cuda.current_stream(dev).cuda_stream
+    st = torch.cuda.Stream(dev)  # explicit: handle 0 would mean the context's own stream
+    sp = st.cuda_stream
+    torch.cuda.set_stream(st)
     d_in = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
     d_out = torch.empty(w * h * 3 // 2, dtype=torch.uint8, device=dev)
     d_pay = torch.empty(cap, dtype=torch.uint8, device=dev)
@@ -53,10 +55,26 @@ def main():
             rc = repr(e)
     stats = codec.kernel_stats()
     ok = bytes(d_out.cpu().numpy()) == expect
+    # wall time per call on the stream (no per-kernel stamps): compress alone,
+    # then the round trip (kernels of one call may run on two streams)
+    codec.profile(False)
+    walls = []
+    for rt in (False, True):
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(steps):
+            codec.compress_device(d_in.data_ptr(), w, h, q, d_pay.data_ptr(), cap, d_size.data_ptr(), sp)
+            if rt:
+                codec.decompress_device(d_pay.data_ptr(), d_size.data_ptr(), cap, w, h, q, d_out.data_ptr(), sp)
+        t1.record()
+        torch.cuda.synchronize()
+        walls.append(t0.elapsed_time(t1) / steps * 1e3)
     print(f"{os.environ.get('MYYUV_HIP_LIB', 'default')} {w}x{h} q{q[0]}: rc={rc} roundtrip_equal={ok}")
     for k, (ms, n) in stats.items():
         if n:
             print(f"  {k:14s} {ms / n * 1e3:9.2f} us")
+    print(f"  compress wall    {walls[0]:9.2f} us")
+    print(f"  round trip wall  {walls[1]:9.2f} us")
     codec.close()
 
 
