@@ -130,30 +130,45 @@ __host__ __device__ __forceinline__ uint32_t coef_quad(uint32_t g, uint32_t c) {
   return ((g >> 6) * 8u + c) * 64u + (g & 63u);
 }
 
-// K2 -> K4 hand-off, per batch tile T:
-//   stage:  T * kTileCap bytes, one kWaveRun-byte region per K2 wave: the
-//           chunks of the wave's blocks with at most 8 distinct symbols, back
-//           to back in the wave's (class-sorted) order (a "dense run");
-//   srcoff: u16 per block: the chunk's byte offset in its tile's stage
-//           region, kSrcOverflow for a block with more symbols, whose chunk
-//           the overflow passes write to oslots at g * kMaxChunk;
+// K2 works on windows of kWinTiles consecutive batch tiles (window w = batch
+// tiles [w * kWinTiles, (w + 1) * kWinTiles)): one workgroup classifies the
+// window's blocks and sorts them by class over the whole window, so its 64-block
+// runs are more uniform than a single tile's would be.
+#ifndef MYYUV_K2_WIN
+#define MYYUV_K2_WIN 4
+#endif
+constexpr uint32_t kWinTiles = MYYUV_K2_WIN;
+static_assert((kWinTiles & (kWinTiles - 1)) == 0 && kWinTiles >= 1 && kWinTiles <= 8, "kWinTiles: 1, 2, 4 or 8");
+__host__ __device__ __forceinline__ uint32_t win_first_tile(uint32_t T) { return T & ~(kWinTiles - 1u); }
+
+// K2 -> K4 hand-off, per window of batch tiles:
+//   stage:  kTileCap bytes per batch tile (the window's tiles' regions are
+//           contiguous), one kWaveRun-byte region per 64-block run: the chunks
+//           of the run's blocks with at most 8 distinct symbols, back to back
+//           in the run's (class-sorted) order (a "dense run");
+//   srcoff: u32 per block: the chunk's byte offset from its window's first
+//           tile's stage region, kSrcOverflow for a block with more symbols,
+//           whose chunk the overflow passes write to oslots at g * kMaxChunk;
 //   tinfo:  kTInfoWords u32 per tile: [0] overflow chunk bytes (the overflow
-//           passes add to it), [1 .. 4] dense-run bytes of K2's waves 0..3,
-//           [8] the tile's exclusive prefix in its frame's content
-//           (k_tile_scan).
+//           passes add to it), [1 .. 4] the tile's dense-chunk bytes (k_huff_encode:
+//           all in [1]; k_encode_tile: per wave), [8] the tile's exclusive
+//           prefix in its frame's content (k_tile_scan).
 constexpr uint32_t kTileCap = kK2Group * kMaxChunk;
 constexpr uint32_t kWaveRun = kWave * kMaxChunk;
 constexpr uint32_t kTInfoWords = 16;
 constexpr uint32_t kTInfoPrefix = 8;
-constexpr uint16_t kSrcOverflow = 0xFFFF;
+constexpr uint32_t kSrcOverflow = 0xFFFFFFFFu;
 // The hand-off is laid out for exactly four K2 waves per tile: k_tile_scan sums
 // tinfo words 1..4, k_stream_out keeps four run totals, k_encode_tile's
 // phase 1 covers 4 waves x 4 units x 16 blocks, and tinfo word kTInfoPrefix
-// must lie past the run words; a tile's byte offsets must fit srcoff's u16
-// below kSrcOverflow.
+// must lie past the run words.
 static_assert(kK2Group == 4 * kWave, "the K2 -> K4 hand-off assumes 4 waves per tile");
 static_assert(1 + kK2Group / kWave <= kTInfoPrefix, "tinfo run words overlap the tile prefix");
-static_assert(kTileCap <= kSrcOverflow, "tile offsets must fit the u16 srcoff below kSrcOverflow");
+
+// Batch tiles rounded up to whole windows (the stage buffer's extent).
+__host__ __device__ __forceinline__ uint32_t win_tiles_alloc(uint32_t ntiles) {
+  return (ntiles + kWinTiles - 1u) & ~(kWinTiles - 1u);
+}
 
 // Plane, first block (frame-local) and block count of tile t of a frame.
 __host__ __device__ __forceinline__ int tile_plane(const FrameGeom& G, uint32_t t) {

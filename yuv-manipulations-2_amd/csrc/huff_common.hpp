@@ -661,17 +661,18 @@ MYYUV_HD uint32_t block_class(const CoefRegs& R, int msz) {
 // coefficient alone; Huffman.cpp:191-194 for the all-zero case): one code of
 // length 1, one table group; the chunk is 7 bytes:
 //   u16 nbits = 1, u8 table_bytes = 3, group header 0x00, 11-bit key, 1 code byte 0.
-MYYUV_HD void build_single(const CoefRegs& R, EncState& S) {
+MYYUV_HD void build_single_dc(int dc, EncState& S) {
   S.hdr = 1u | (3u << 16);
   S.size = 7;
   S.n = 1;
   S.msz = 1;
   S.lcount = 1;
-  S.TK[0] = ((uint32_t)R.sym(0) & 0x7FFu) | (1u << 11);
+  S.TK[0] = ((uint32_t)dc & 0x7FFu) | (1u << 11);
   S.TK[1] = S.TK[2] = S.TK[3] = 0u;
   S.cc = 0;  // slot 0: code 0,
   S.ll = 1;  // length 1
   S.ids.clear();
 }
+MYYUV_HD void build_single(const CoefRegs& R, EncState& S) { build_single_dc(R.sym(0), S); }
 
 }  // namespace myyuv_gpu

@@ -814,7 +814,7 @@ struct TileScratch {
 template <class Src>
 __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uint32_t T, uint32_t nloc,
                                             uint32_t* __restrict__ stage, uint32_t* __restrict__ tinfo,
-                                            uint8_t* __restrict__ sizes, uint16_t* __restrict__ srcoff,
+                                            uint8_t* __restrict__ sizes, uint32_t* __restrict__ srcoff,
                                             uint32_t* __restrict__ work, uint32_t* __restrict__ work_count) {
   constexpr int kWaves = kTileWaves;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -914,7 +914,7 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
     emit_chunk(S, wmsz, dw);
     dw.finish(above ? (nhdr | 0x80000000u) : 0u);
     sizes[mg] = (uint8_t)S.size;
-    srcoff[mg] = (uint16_t)(wave * kWaveRun + off);
+    srcoff[mg] = (T & (kWinTiles - 1u)) * kTileCap + wave * kWaveRun + off;  // from the window's first tile
   }
   // blocks with more than 8 distinct symbols: the overflow passes' worklist
   const uint64_t ovf = __ballot(live && !ok);
@@ -932,8 +932,82 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
 
 }  // namespace
 
-// K2 over K1's coefficients in HBM: one workgroup per tile (grid (tiles, frames)).
+namespace {
+
+// K2's window sort (k_huff_encode): the window's blocks are counting-sorted
+// by class (dead slots last) over kWinTiles tiles at once.  Sort slots are
+// the (tile round, wave) pairs that classified them, so the order is stable:
+// class, then window slot (tile, block).
+constexpr uint32_t kWinBlocks = kWinTiles * kK2Group;
+constexpr uint32_t kWinRuns = kWinBlocks / kWave;  // 64-block runs per window
+// sort keys: the single class, then each of the other classes split by
+// message length (<= 8, <= 16, longer: the per-position loops run to the
+// run's longest message), the dead slots last
+#ifndef MYYUV_K2_MSZ_SPLIT
+#define MYYUV_K2_MSZ_SPLIT 1
+#endif
+constexpr uint32_t kMszBuckets = MYYUV_K2_MSZ_SPLIT ? 3 : 1;
+constexpr uint32_t kKeys = 2 + (kClassDead - 1) * kMszBuckets;
+constexpr uint32_t kDeadKey = kKeys - 1;
+__device__ __forceinline__ uint32_t sort_key(uint32_t cls, uint32_t msz) {
+  if (cls == kClassDead) return kDeadKey;
+  if (cls == kClassSingle) return 0;
+  const uint32_t b = kMszBuckets == 1 ? 0u : (msz > 8 ? 1u : 0u) + (msz > 16 ? 1u : 0u);
+  return 1 + (cls - 1) * kMszBuckets + b;
+}
+constexpr uint32_t kScanVals = kKeys * kWinRuns;  // [key][round * 4 + wave] counts
+constexpr uint32_t kScanPer = (kScanVals + kWave - 1) / kWave;
+static_assert(kK2Group == 256, "window slots are tile << 8 | block");
+
+// set bits of m below the calling lane (v_mbcnt: no 64-bit lane mask held)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The lane id through an opaque (volatile) v_mbcnt pair: never hoisted out
+// of a loop nor merged with another evaluation.
+__device__ __forceinline__ uint32_t fresh_lane_id() {
+  uint32_t lo, id;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0" : "=v"(lo));
+  asm volatile("v_mbcnt_hi_u32_b32 %0, -1, %1" : "=v"(id) : "v"(lo));
+  return id;
+}
+__device__ __forceinline__ int wave_max_ln(int v, uint32_t ln) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) v = max(v, __builtin_amdgcn_ds_bpermute((int)((ln ^ (uint32_t)d) << 2), v));
+  return v;
+}
+
+struct WinScratch {
+  uint16_t slot[kWinBlocks];  // sorted position -> window slot (tile << 8 | block)
+  uint8_t msz[kWinBlocks], cls[kWinBlocks], rm[kWinBlocks];
+  uint32_t cnt[kScanVals];    // per (key, sort slot): count, then exclusive position
+  uint32_t gb[kWinTiles];     // batch-global index of tile k's block 0
+  uint32_t tot[kWinTiles];    // tile k's dense chunk bytes
+  uint32_t next, done, ntl;   // run counter, finished waves, the window's tiles
+};
+
+}  // namespace
+
+// K2 over K1's coefficients in HBM: one workgroup per window of kWinTiles
+// batch tiles (grid: windows).
 //   coef: natural-order quads (codec_common.hpp); sizes: [n] u8.
+// 1. classify: thread i takes block i of each of the window's tiles (one
+//    coefficient load per block, coalesced), its message length and class;
+// 2. a counting sort of the window's blocks by class (ballot ranks per round
+//    and wave, one wave scans the counts);
+// 3. the sorted blocks in 64-block runs, heaviest run first, taken by the
+//    waves from an LDS counter (no barrier between runs: a wave that drew
+//    light runs takes more of them).  Each lane builds its block's code, a
+//    wave scan places the chunks back to back in the run's stage region
+//    (DenseWriter), srcoff records where, and the run's chunk bytes are added
+//    to their tiles' totals in LDS; blocks with more than 8 distinct symbols
+//    go to the overflow worklist;
+// 4. the last wave to finish publishes the tiles' totals (tinfo word 1).
+// Sorting over 4 tiles rather than one makes the runs more uniform: per
+// 4032x3008 frame the waves' class mix (single / <= 4 / <= 8 / rest) drops
+// from 1859 / 834 / 740 / 1010 runs to 2220 / 968 / 652 / 603
+// (tools/k2_window_sim.py).
 #ifndef MYYUV_K2_WAVES
 #define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (12 spilled; 6 measured +1.5 % before the emit tables, −1 % after: its spills grew; tools/ab_bench.sh, tools/kus_ab.sh)
 #endif
@@ -943,16 +1017,202 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
                                                          uint32_t* __restrict__ stage,
                                                          uint32_t* __restrict__ tinfo,
                                                          uint8_t* __restrict__ sizes,
-                                                         uint16_t* __restrict__ srcoff,
+                                                         uint32_t* __restrict__ srcoff,
                                                          uint32_t* __restrict__ work,
                                                          uint32_t* __restrict__ work_count) {
-  __shared__ TileScratch sc;
-  const uint32_t t = blockIdx.x, f = blockIdx.y;
-  const int p = tile_plane(G, t);
-  const uint32_t g0 = tile_first(G, p, t);
-  const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
-  const GlobalCoef src{coef, rmask, zq, f * G.cum[3] + g0};
-  encode_tile(src, sc, f * G.tcum[3] + t, nloc, stage, tinfo, sizes, srcoff, work, work_count);
+  __shared__ WinScratch sc;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t NT = G.nframes * G.tcum[3];
+  const uint32_t T0 = blockIdx.x * kWinTiles;
+  // ---- the window's tiles (wave-uniform)
+  uint32_t gbk[kWinTiles], nlk[kWinTiles];
+#pragma unroll
+  for (uint32_t k = 0; k < kWinTiles; k++) {
+    const uint32_t T = T0 + k;
+    nlk[k] = 0;
+    gbk[k] = 0;
+    if (T < NT) {
+      const uint32_t f = G.nframes > 1 ? T / G.tcum[3] : 0u;
+      const uint32_t t = T - f * G.tcum[3];
+      const int p = tile_plane(G, t);
+      const uint32_t g0 = tile_first(G, p, t);
+      nlk[k] = min(kK2Group, G.cum[p + 1] - g0);
+      gbk[k] = f * G.cum[3] + g0;
+    }
+  }
+  if (tid < kWinTiles) {
+    sc.gb[tid] = gbk[tid];
+    sc.tot[tid] = 0;
+    // the overflow passes add their chunk bytes to the tile's info word 0
+    // (ordered before them by the kernel boundary)
+    if (T0 + tid < NT) tinfo[(size_t)(T0 + tid) * kTInfoWords] = 0u;
+  }
+  if (tid == 0) {
+    sc.next = 0;
+    sc.done = 0;
+    sc.ntl = min(kWinTiles, NT - T0);
+  }
+  // ---- 1. classify, with per-round ballot ranks
+  uint32_t ent[kWinTiles];  // per round: class | msz << 3 | row mask << 10 | rank << 18
+  uint32_t rmv[kWinTiles];
+#pragma unroll
+  for (uint32_t k = 0; k < kWinTiles; k++) rmv[k] = tid < nlk[k] ? rmask[gbk[k] + tid] : 0u;
+  // round k + 1's coefficients are loaded before round k is classified
+  CoefRegs RR[2];
+  RR[0].load(coef, zq, tid < nlk[0] ? gbk[0] + tid : 0u, rmv[0]);
+#pragma unroll
+  for (uint32_t k = 0; k < kWinTiles; k++) {
+    if (k + 1 < kWinTiles)
+      RR[(k + 1) & 1].load(coef, zq, tid < nlk[(k + 1) % kWinTiles] ? gbk[(k + 1) % kWinTiles] + tid : 0u,
+                           rmv[(k + 1) % kWinTiles]);
+    uint32_t cls = kClassDead, m = 0;
+    const uint32_t rm = rmv[k];
+    if (tid < nlk[k]) {
+      const int msz = RR[k & 1].msz();
+      m = (uint32_t)msz;
+      cls = block_class(RR[k & 1], msz);
+    }
+    const uint32_t key = sort_key(cls, m);
+    uint32_t rk = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kKeys; c++) {
+      const uint64_t b = __ballot(key == c);
+      if (key == c) rk = lanes_below(b);
+      if (lane == 0) sc.cnt[c * kWinRuns + k * kTileWaves + wave] = (uint32_t)__popcll(b);
+    }
+    ent[k] = cls | (m << 3) | (rm << 10) | (rk << 18) | (key << 24);
+  }
+  __syncthreads();
+  // ---- 2. exclusive scan of the counts in (key, round, wave) order (wave 0)
+  if (wave == 0) {
+    uint32_t v[kScanPer], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; j++) {
+      const uint32_t idx = lane * kScanPer + j;
+      v[j] = idx < kScanVals ? sc.cnt[idx] : 0u;
+      sum += v[j];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
+      if (lane >= (uint32_t)d) incl += o;
+    }
+    uint32_t ex = incl - sum;
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; j++) {
+      const uint32_t idx = lane * kScanPer + j;
+      if (idx < kScanVals) sc.cnt[idx] = ex;
+      ex += v[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kWinTiles; k++) {
+    const uint32_t x = ent[k];
+    const uint32_t pos = sc.cnt[(x >> 24) * kWinRuns + k * kTileWaves + wave] + ((x >> 18) & 63u);
+    sc.slot[pos] = (uint16_t)((k << 8) | tid);
+    sc.msz[pos] = (uint8_t)((x >> 3) & 127u);
+    sc.cls[pos] = (uint8_t)(x & 7u);
+    sc.rm[pos] = (uint8_t)(x >> 10);
+  }
+  // the live blocks = the exclusive position of the first dead slot
+  const uint32_t nlive = sc.cnt[kDeadKey * kWinRuns];
+  __syncthreads();
+  const uint32_t nruns = (nlive + kWave - 1) / kWave;
+  // ---- 3. the runs, heaviest first
+  while (true) {
+    uint32_t r = 0;
+    if (lane == 0) r = atomicAdd(&sc.next, 1u);
+    r = (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
+    if (r >= nruns) break;
+    const uint32_t run = nruns - 1 - r;
+    // the lane id, recomputed per run (opaque to the optimiser): kept out of
+    // the loop, every lane-derived address (shuffles, LDS) would be hoisted
+    // and held in registers across the run's encoder, which then spills
+    const uint32_t ln = fresh_lane_id();
+    const uint32_t e = run * kWave + ln;
+    const uint32_t sl = sc.slot[e];
+    const int mm = sc.msz[e];
+    const uint32_t mc = sc.cls[e];
+    const uint32_t mrm = sc.rm[e];
+    const bool live = e < nlive;
+    const uint32_t k = sl >> 8;
+    const uint32_t mg = sc.gb[k] + (sl & 255u);
+    uint32_t wcls = kClassDead;  // the run's heaviest class
+#pragma unroll
+    for (int c = kClassDead - 1; c >= 0; c--)
+      if (wcls == kClassDead && __ballot(live && mc == (uint32_t)c) != 0) wcls = (uint32_t)c;
+    const int wmsz = max(wave_max_ln(live ? mm : 0, ln), 1);
+    EncState S;
+    bool ok = false;
+    // (the coefficients are loaded inside each class's branch: loaded before
+    // it, they are spilled to scratch across the branch, one dependent load
+    // round trip per quad)
+    if (wcls == kClassSingle) {
+      // one symbol: the DC coefficient (word 0 of quad 0), or 0
+      const uint32_t dc = (live && (mrm & 1u)) ? reinterpret_cast<const uint32_t*>(coef)[coef_quad(mg, 0) * 4u] : 0u;
+      if (live) {
+        build_single_dc((int)(int16_t)dc, S);
+        ok = true;
+      }
+    } else if (wcls == kClassR4) {
+      CoefRegs R;
+      R.load(coef, zq, live ? mg : 0u, live ? mrm : 0u);
+      if (live) ok = build_r<4>(R, mm, wmsz, S);
+    } else {
+      CoefRegs R;
+      R.load(coef, zq, live ? mg : 0u, live ? mrm : 0u);
+      if (live) ok = build_r<8>(R, mm, wmsz, S);
+    }
+    // the run's chunks back to back (offsets by a wave scan of the sizes),
+    // every dword stored once (DenseWriter)
+    const bool dense = live && ok;
+    const uint32_t sz = dense ? S.size : 0u;
+    uint32_t incl = sz;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ln - (uint32_t)d) << 2), (int)incl);
+      if (ln >= (uint32_t)d) incl += o;
+    }
+    const uint32_t off = incl - sz;
+    const uint64_t dm = __ballot(dense);
+    const uint64_t above = ln == 63 ? 0ull : dm & ~((2ull << ln) - 1ull);
+    const int nl = above ? __ffsll((long long)above) - 1 : (int)ln;
+    const uint32_t nhdr = (uint32_t)__builtin_amdgcn_ds_bpermute(nl << 2, (int)(dense ? S.hdr : 0u));
+    if (dense) {
+      DenseWriter dw;
+      dw.init(stage + ((size_t)blockIdx.x * kWinTiles * (kTileCap / 4) + run * (kWaveRun / 4)), off);
+      emit_chunk(S, wmsz, dw);
+      dw.finish(above ? (nhdr | 0x80000000u) : 0u);
+      sizes[mg] = (uint8_t)S.size;
+      srcoff[mg] = run * kWaveRun + off;
+      atomicAdd(&sc.tot[k], S.size);
+    }
+    // blocks with more than 8 distinct symbols: the overflow passes' worklist
+    const uint64_t ovf = __ballot(live && !ok);
+    if (ovf) {
+      if (live && !ok) srcoff[mg] = kSrcOverflow;
+      uint32_t base = 0;
+      if (ln == 0) base = atomicAdd(work_count, (uint32_t)__popcll(ovf));
+      base = __builtin_amdgcn_readfirstlane(base);
+      if ((ovf >> ln) & 1) work[base + lanes_below(ovf)] = mg;
+    }
+  }
+  // ---- 4. the last wave out publishes the tiles' dense bytes
+  uint32_t d = 0;
+  if (lane == 0) d = __hip_atomic_fetch_add(&sc.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  d = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+  if (d == kTileWaves - 1) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (lane < sc.ntl) {
+      uint32_t* info = tinfo + (size_t)(blockIdx.x * kWinTiles + lane) * kTInfoWords;
+      info[1] = __hip_atomic_load(&sc.tot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      info[2] = 0u;
+      info[3] = 0u;
+      info[4] = 0u;
+    }
+  }
 }
 
 // Fused single-pass encoder: K1 + K2 for one tile, the
@@ -1025,7 +1285,7 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
                                                              uint32_t* __restrict__ stage,
                                                              uint32_t* __restrict__ tinfo,
                                                              uint8_t* __restrict__ sizes,
-                                                             uint16_t* __restrict__ srcoff,
+                                                             uint32_t* __restrict__ srcoff,
                                                              uint32_t* __restrict__ work,
                                                              uint32_t* __restrict__ work_count) {
   using namespace xf;

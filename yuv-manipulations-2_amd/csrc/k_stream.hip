@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
 __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__ stage,
                                                     const uint32_t* __restrict__ tinfo,
                                                     const uint8_t* __restrict__ sizes,
-                                                    const uint16_t* __restrict__ srcoff,
+                                                    const uint32_t* __restrict__ srcoff,
                                                     const uint32_t* __restrict__ oslots, FrameGeom G,
                                                     uint8_t* __restrict__ out, uint32_t cap) {
   __shared__ uint32_t s_wt[4], s_hdr[4];
@@ -247,14 +247,14 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
     src = oslots + (size_t)(gb + tid) * kSlotWords;
     sh = 0;
   } else {
-    src = stage + (size_t)T * (kTileCap / 4) + (so >> 2);
+    src = stage + (size_t)win_first_tile(T) * (kTileCap / 4) + (so >> 2);  // (window-relative)
     sh = so & 3u;
   }
   uint32_t nxh = 0;  // the next tile's first header (lane nloc - 1, plane going on)
   if (tid == nloc - 1 && !plane_end) {
     const uint32_t so1 = srcoff[gb + nloc];
     const uint32_t* s1 = so1 == kSrcOverflow ? oslots + (size_t)(gb + nloc) * kSlotWords
-                                             : stage + (size_t)(T + 1) * (kTileCap / 4) + (so1 >> 2);
+                                             : stage + (size_t)win_first_tile(T + 1) * (kTileCap / 4) + (so1 >> 2);
     const uint32_t r1 = so1 == kSrcOverflow ? 0u : so1 & 3u;
     nxh = r1 ? (s1[0] >> (8 * r1)) | (s1[1] << (32 - 8 * r1)) : s1[0];
   }

@@ -30,18 +30,18 @@ __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const S
                               const uint32_t*, FrameGeom, uint32_t, uint32_t, const QTables*, uint4*, uint8_t*,
                               unsigned long long*);
 __global__ void k_huff_encode(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
-                              uint8_t*, uint16_t*, uint32_t*, uint32_t*);
+                              uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
                                    const uint32_t*, const uint32_t*, uint32_t);
 __global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
                                    uint32_t*, const uint32_t*, const uint32_t*, uint32_t);
 __global__ void k_encode_tile(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint32_t*, uint32_t*,
-                              uint8_t*, uint16_t*, uint32_t*, uint32_t*);
+                              uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_tile_scan(uint32_t*, FrameGeom, uint8_t*, uint32_t, uint32_t*, unsigned long long*);
 __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*, uint32_t, FrameGeom,
                              StreamDesc*, uint32_t*, uint32_t*, uint32_t, unsigned long long*,
                              uint32_t, unsigned long long*);
-__global__ void k_stream_out(const uint32_t*, const uint32_t*, const uint8_t*, const uint16_t*,
+__global__ void k_stream_out(const uint32_t*, const uint32_t*, const uint8_t*, const uint32_t*,
                              const uint32_t*, FrameGeom, uint8_t*, uint32_t);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
@@ -311,10 +311,10 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   const uint32_t ntiles = ceil_div(G.cum[3], kScanTile);
   int e = 0;
   e |= c->coef.grow((size_t)nwaves * kCoefQuadsPerWave * 16);  // natural-order quads
-  e |= c->stage.grow((size_t)nf * G.tcum[3] * kTileCap);
+  e |= c->stage.grow((size_t)win_tiles_alloc(nf * G.tcum[3]) * kTileCap);
   e |= c->oslots.grow((size_t)nblk * kMaxChunk);
   e |= c->tinfo.grow((size_t)nf * G.tcum[3] * kTInfoWords * 4);
-  e |= c->srcoff.grow((size_t)nblk * 2);
+  e |= c->srcoff.grow((size_t)nblk * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
   e |= c->rmask.grow((size_t)nblk);
   if (c->zq.n == 0) {
@@ -358,10 +358,10 @@ int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
-  const int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(G.tcum[3], nf), dim3(kK2Group), s,
+  const int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(win_tiles_alloc(nf * G.tcum[3]) / kWinTiles), dim3(kK2Group), s,
                c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
                c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
-               c->srcoff.as<uint16_t>(), list, count);
+               c->srcoff.as<uint32_t>(), list, count);
   return e | launch_overflow(c, G, s);
 }
 
@@ -398,7 +398,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
     e |= hipMemsetAsync(count, 0, 4, s) != hipSuccess;
     e |= launch(c, MYYUV_K_ENCODE_TILE, k_encode_tile, dim3(G.tcum[3], nf), dim3(kK2Group), s,
                 static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
-                c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(), c->srcoff.as<uint16_t>(),
+                c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(), c->srcoff.as<uint32_t>(),
                 count + 64, count);
     e |= launch_overflow(c, G, s);
   } else {
@@ -413,7 +413,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
               static_cast<uint8_t*>(d_out), cap, d_size, err);
   e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
               c->stage.as<const uint32_t>(), c->tinfo.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
-              c->srcoff.as<const uint16_t>(), c->oslots.as<const uint32_t>(), G, static_cast<uint8_t*>(d_out),
+              c->srcoff.as<const uint32_t>(), c->oslots.as<const uint32_t>(), G, static_cast<uint8_t*>(d_out),
               cap);
   return e ? MYYUV_E_HIP : 0;
 }
@@ -1084,11 +1084,11 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   // K2's hand-off (codec_common.hpp): per tile the waves' dense runs, the
   // chunks of blocks with more than 8 symbols in their own slots
   const uint32_t ntile = G.tcum[3];
-  std::vector<uint8_t> stage((size_t)ntile * kTileCap), oslots((size_t)nblocks * kMaxChunk);
-  std::vector<uint16_t> soff(nblocks);
+  std::vector<uint8_t> stage((size_t)win_tiles_alloc(ntile) * kTileCap), oslots((size_t)nblocks * kMaxChunk);
+  std::vector<uint32_t> soff(nblocks);
   if (hipMemcpyAsync(stage.data(), c->stage.p, stage.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipMemcpyAsync(oslots.data(), c->oslots.p, oslots.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(soff.data(), c->srcoff.p, (size_t)nblocks * 2, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(soff.data(), c->srcoff.p, (size_t)nblocks * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipMemcpyAsync(sizes, c->sizes.p, nblocks, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return MYYUV_E_HIP;
@@ -1096,7 +1096,7 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
     uint8_t* dst = chunks160 + (size_t)g * kMaxChunk;
     std::memset(dst, 0, kMaxChunk);
     const uint8_t* src = soff[g] == kSrcOverflow ? oslots.data() + (size_t)g * kMaxChunk
-                                                 : stage.data() + (size_t)(g / kK2Group) * kTileCap + soff[g];
+                                                 : stage.data() + (size_t)win_first_tile(g / kK2Group) * kTileCap + soff[g];
     std::memcpy(dst, src, sizes[g]);
   }
   return 0;
