@@ -657,6 +657,56 @@ MYYUV_HD uint32_t block_class(const CoefRegs& R, int msz) {
   return nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// block_class and CoefRegs::msz on the device in packed 16-bit arithmetic:
+// per coefficient pair, the nonzero flags min(v, 1) (v_pk_min_u16), their
+// running count (v_pk_add_u16) and the running maximum of flag * (zig-zag
+// index + 1) (v_pk_max_u16): five instructions per pair where the scalar
+// forms take about ten.  Same results as the host forms.
+typedef unsigned short myyuv_us2 __attribute__((ext_vector_type(2)));
+struct ZzPairs {
+  uint32_t v[32];  // natural pair w: (zig-zag index + 1) of coefficients 2w, 2w+1
+  constexpr ZzPairs() : v{} {
+    uint32_t inv[64] = {};
+    for (int i = 0; i < 64; i++) inv[c_zz[i]] = (uint32_t)i + 1u;
+    for (int w = 0; w < 32; w++) v[w] = inv[2 * w] | (inv[2 * w + 1] << 16);
+  }
+};
+constexpr ZzPairs kZzPairs{};
+__device__ __forceinline__ void block_class_msz(const CoefRegs& R, int& msz, uint32_t& cls) {
+  myyuv_us2 cnt = {0, 0}, mx = {0, 0};
+#pragma unroll
+  for (int w = 0; w < 32; w++) {
+    // (asm: the compiler rewrites min(x, 1) as two compares and selects)
+    uint32_t fu;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(fu) : "v"(R.w[w]), "s"(0x00010001u));
+    const myyuv_us2 f = __builtin_bit_cast(myyuv_us2, fu);
+    cnt += f;
+    // flag * index without the packed multiply (VOP3P takes no literal: its 32
+    // index constants would sit in SGPRs): a per-half all-ones mask 0 - flag
+    // (asm: the compiler turns it into a 32-bit multiply), then AND with the
+    // literal pair
+    uint32_t m16;
+    asm("v_pk_sub_u16 %0, 0, %1" : "=v"(m16) : "v"(fu));
+    mx = __builtin_elementwise_max(mx, __builtin_bit_cast(myyuv_us2, m16 & kZzPairs.v[w]));
+  }
+  const uint32_t nnz = (uint32_t)cnt.x + (uint32_t)cnt.y;
+  const int m = (int)(mx.x > mx.y ? mx.x : mx.y);
+  msz = m;
+  if (m <= 1) {
+    cls = kClassSingle;
+  } else {
+    const uint32_t nub = nnz + ((uint32_t)m > nnz ? 1u : 0u);
+    cls = nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
+  }
+}
+#else
+MYYUV_HD void block_class_msz(const CoefRegs& R, int& msz, uint32_t& cls) {
+  msz = R.msz();
+  cls = block_class(R, msz);
+}
+#endif
+
 // Blocks whose message is one symbol (msz <= 1: all zero, or the DC
 // coefficient alone; Huffman.cpp:191-194 for the all-zero case): one code of
 // length 1, one table group; the chunk is 7 bytes:

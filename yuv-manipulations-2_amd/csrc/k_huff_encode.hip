@@ -1068,9 +1068,9 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     uint32_t cls = kClassDead, m = 0;
     const uint32_t rm = rmv[k];
     if (tid < nlk[k]) {
-      const int msz = RR[k & 1].msz();
+      int msz;
+      block_class_msz(RR[k & 1], msz, cls);
       m = (uint32_t)msz;
-      cls = block_class(RR[k & 1], msz);
     }
     const uint32_t key = sort_key(cls, m);
     uint32_t rk = 0;
@@ -1120,6 +1120,9 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   const uint32_t nlive = sc.cnt[kDeadKey * kWinRuns];
   __syncthreads();
   const uint32_t nruns = (nlive + kWave - 1) / kWave;
+#if defined(MYYUV_K2_EXP) && MYYUV_K2_EXP == 1
+  if (nruns < 1000000u) return;  // diagnostic: classify + sort only
+#endif
   // ---- 3. the runs, heaviest first
   while (true) {
     uint32_t r = 0;
