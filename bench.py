@@ -5,13 +5,13 @@ Workloads (--workload; `auto`, the default, picks chef-big at one rank and
 batch4k at more):
   chef-big  BASELINE.json configs[1], the metric's own configuration: a step
             is one DCT compress + decompress round trip of --inflight x
-            --batch (default 3 x 7 = 21) 4032x3008 IYUV frames per rank
+            --batch (default 4 x 8 = 32) 4032x3008 IYUV frames per rank
             (chef-with-trumpet-big, q=50; its raw input is missing from the
             reference, so the frame is the sha-pinned decode of
             chef-with-trumpet-big-DCT-50.myyuv), read from --input-frames
-            (default 24, rounded down to a multiple of --batch) distinct HBM
-            copies: more bytes than the 256 MiB Infinity Cache, so the pixel
-            reads come from HBM.  Weak scaling: every rank runs that batch.
+            (default: one per frame of a step, at least 24, rounded down to a
+            multiple of --batch) distinct HBM copies: more bytes than the 256
+            MiB Infinity Cache, so the pixel reads come from HBM.  Weak scaling: every rank runs that batch.
   batch4k   BASELINE.json configs[3]/[4]: a step is the batch of --frames
             (default 512) synthetic 3840x2160 IYUV frames, q=50 (frame f: the
             tiled chef-big frame with origin (8f mod 4032, 8f mod 3008),
@@ -132,11 +132,11 @@ def parse(argv=None):
                     help="event-stamp K1 on launch group 0 only (default: every group's K1 launches)")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the step without K1's HIP events (no roofline)")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="launch groups in flight per GPU, each on its own codec context and HIP stream "
                          "(1 = strictly serial)")
     ap.add_argument("--batch", type=int, default=0,
-                    help="frames per launch (the batch entry points; 0 = 7 for chef-big, 8 for batch4k)")
+                    help="frames per launch (the batch entry points; 0 = 8)")
     ap.add_argument("--stream-priority", default="",
                     help="comma-separated HIP stream priorities of the launch groups' streams "
                          "(cycled; default all normal)")
@@ -148,10 +148,10 @@ def parse(argv=None):
                     help="round trips of the host-buffer API side measurement (0 disables it)")
     ap.add_argument("--breakdown-steps", type=int, default=5,
                     help="untimed launch groups after the timed region with every kernel stamped")
-    ap.add_argument("--input-frames", type=int, default=24,
+    ap.add_argument("--input-frames", type=int, default=0,
                     help="chef-big: distinct HBM copies of the input frame the launch groups read in turn "
-                         "(24 x 18.2 MB = 436 MB: larger than the 256 MiB Infinity Cache; rounded "
-                         "down to a multiple of --batch: 21 copies, 382 MB, at the default 7)")
+                         "(0: one per frame of a step, at least 24; rounded down to a multiple of --batch: "
+                         "32 copies, 582 MB at the default 4 x 8, larger than the 256 MiB Infinity Cache)")
     ap.add_argument("--cpu-codec", action="store_true",
                     help="tests only: the CPU restatement as the codec, host tensors, gloo (no GPU)")
     ap.add_argument("--launch-selftest", action="store_true",
@@ -485,12 +485,13 @@ class Run:
         self.verified = {}
         if name == "chef-big":
             self.w, self.h = big.width, big.height
-            self.B = args.batch or 7
+            self.B = args.batch or 8
             self.per_step = self.nf * self.B
             self.n_local = self.per_step
             self.n_total = world * self.per_step
             self.cap = SLOT_4K if isinstance(codec, CpuCodec) else None
-            nin = max(self.B, (max(args.input_frames, self.B) // self.B) * self.B)
+            want = args.input_frames or max(24, self.per_step)
+            nin = max(self.B, (max(want, self.B) // self.B) * self.B)
             self.nin = nin
             self.samples = self.w * self.h * 3 // 2
             self.d_in = codec.empty((nin, self.samples))
