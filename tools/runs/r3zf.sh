@@ -1,0 +1,12 @@
+# K2: rest-class blocks with >= 13 nonzero coefficients straight to the overflow worklist (in-tree;
+# dn0 = off, dn11 / dn16 = other thresholds)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r3zf_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r3zf_tests.log; exit 1; }
+tail -1 gpurun_out/r3zf_tests.log
+timeout -k 10 300 python3 tools/k1_ab.py build_var/dn0 default build_var/dn11 build_var/dn16 > gpurun_out/r3zf_kernels.txt 2>&1 || { echo KAB_FAILED; tail -20 gpurun_out/r3zf_kernels.txt; exit 1; }
+cat gpurun_out/r3zf_kernels.txt
+timeout -k 10 500 bash tools/ab_bench.sh build_var/base build_var/dn0 default build_var/dn11 build_var/dn16 > gpurun_out/r3zf_ab.txt 2>&1 || { echo AB_FAILED; tail -20 gpurun_out/r3zf_ab.txt; exit 1; }
+cp gpurun_out/ab_bench.txt gpurun_out/r3zf_ab.txt
+cat gpurun_out/r3zf_ab.txt
