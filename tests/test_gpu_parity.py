@@ -127,6 +127,35 @@ def test_sparse_blocks_vs_oracle(codec, oracle, q):
     assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q)
 
 
+def flat_block_frame(w, h, seed, busy):
+    """IYUV frame of flat 8x8 blocks (every value 0..255 occurs: DC-only blocks
+    over the whole DC range), with a `busy` share of blocks, at random
+    positions, carrying noise (blocks with AC coefficients between them)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for pw, ph in ((w, h), (w // 2, h // 2), (w // 2, h // 2)):
+        nb = (pw // 8) * (ph // 8)
+        vals = np.resize(rng.permutation(256), nb).astype(np.float64)
+        blk = np.repeat(vals[:, None], 64, 1)
+        noisy = rng.random(nb) < busy
+        blk[noisy] += rng.normal(0, 24, (int(noisy.sum()), 64))
+        img = np.clip(np.rint(blk), 0, 255).astype(np.uint8)
+        out.append(img.reshape(ph // 8, pw // 8, 8, 8).transpose(0, 2, 1, 3).reshape(-1))
+    return np.concatenate(out).tobytes()
+
+
+@pytest.mark.parametrize("q,busy", [((1, 1, 1), 0.0), ((50, 50, 50), 0.3), ((97, 97, 97), 0.1),
+                                    ((100, 100, 100), 0.5), ((3, 60, 100), 0.02)])
+def test_dc_blocks_vs_oracle(codec, oracle, q, busy):
+    """The fused decoder's DC-only blocks (constant rows) and its compacted
+    units of the other blocks, across the DC range and mixes of both."""
+    w, h = 512, 256
+    fr = flat_block_frame(w, h, int(busy * 100) + sum(q), busy)
+    pay = oracle.compress(fr, w, h, q)
+    assert codec.compress(fr, w, h, q) == pay
+    assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q)
+
+
 @pytest.mark.parametrize("wh", [(16, 16), (48, 16), (16, 48), (1008, 16), (144, 272)])
 def test_odd_geometries(codec, oracle, wh):
     w, h = wh

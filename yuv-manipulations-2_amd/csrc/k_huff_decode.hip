@@ -61,6 +61,7 @@ constexpr uint32_t kStageQuads = 384;
 #endif
 
 
+
 struct ZzTable {
   uint8_t v[64];
   constexpr ZzTable() : v{} {
@@ -487,6 +488,7 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
   static_assert(sizeof(uint4) * kStageQuads >= sizeof(float) * xf::kXfTile16, "the tile over the stage");
   __shared__ uint4 stq[kStageQuads];
   __shared__ float sq[64];
+  __shared__ uint16_t s_blk[64];
   const uint32_t lane = threadIdx.x;
   {
     const uint32_t t = blockIdx.x;
@@ -519,7 +521,16 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     return;
   }
 #endif
-  // ---- K6 on the group, unit by unit
+  // ---- K6 on the group.  Blocks whose only nonzero coefficient is the DC
+  // (53 % of the bench frame's blocks) decode to one constant pixel value:
+  // with Z[0][0] = z the only nonzero coefficient, stage 1 leaves U[i][0] =
+  // fl(D[0][i] * z), stage 2 R[i][v] = fl(U[i][0] * D[0][v]) (the other
+  // products are +-0 and every sum starts at +0), and row 0 of the literal
+  // basis is one value c, so R = fl(fl(c * z) * c) for all 64 pixels — the
+  // same two roundings as the full transform, which the lane evaluates for its
+  // own block and stores as 8 rows.  The other blocks are compacted into
+  // 16-block units for K6's transform (one to four units instead of always
+  // four; their rows are written wherever the blocks lie).
   const int p = D.p;
   xf::Unit U;
   U.p = p;
@@ -530,23 +541,57 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
   U.bw = p == 0 ? G.bw[0] : (p == 1 ? G.bw[1] : G.bw[2]);
   U.bmag = p == 0 ? G.bmag[0] : (p == 1 ? G.bmag[1] : G.bmag[2]);
   U.local0 = 0;
+  uint8_t* fr = frame + (size_t)D.f * G.fbytes;
+  uint32_t acc = nw[0] & 0xFFFF0000u;
+#pragma unroll
+  for (int w = 1; w < 32; w++) acc |= nw[w];
+  const bool isdc = D.live && acc == 0u;
+  if (isdc) {
+    constexpr float c0 = xf::c_dct[0];
+    static_assert(xf::c_dct[0] == xf::c_dct[1] && xf::c_dct[0] == xf::c_dct[7], "row 0 of the basis is one value");
+    const float z = (float)(int16_t)nw[0] * sq[0];  // dequantise (DCT.cpp:331)
+    const float u = 0.0f + c0 * z;                  // stage 1: the k = 0 term
+    float S = 0.0f + u * c0;                        // stage 2: the k = 0 term
+    S = __builtin_amdgcn_fmed3f(S, -128.0f, 127.0f);  // (as idct_rows, DCT.cpp:358-362)
+    uint32_t px = xf::bits(S + xf::kMagicPx);
+    if (__builtin_amdgcn_fractf(S) == 0.5f)
+      px = (uint32_t)((int)__builtin_truncf(S + __builtin_copysignf(xf::kHalfDown, S)) + 128);
+    const uint32_t v4 = (px & 0xFFu) * 0x01010101u;
+    const uint2 row = make_uint2(v4, v4);
+#pragma unroll
+    for (uint32_t r = 0; r < 8; r++) {
+      const uint32_t off = xf::block_row_offset(U, D.g - U.cum, r);
+      *reinterpret_cast<uint2*>(fr + off) = row;
+    }
+  }
+  // (compacted in block order: ordering the units by sparsity kind — row 0
+  // only, column 0 only, the rest — measured no faster, profiles/r3zl_*)
+  const uint64_t rest = __ballot(D.live && !isdc);
+  const uint32_t nrest = (uint32_t)__popcll(rest);
+  const uint32_t rrank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rest >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rest, 0u));
+  if (D.live && !isdc) s_blk[rrank] = (uint16_t)lane;  // compacted position -> the block's lane in the group
   float* tile = reinterpret_cast<float*>(stq);
   const uint32_t q = lane & 3u, b = lane >> 2;
-  uint8_t* fr = frame + (size_t)D.f * G.fbytes;
 #pragma unroll 1
-  for (uint32_t u = 0; u < 4; u++) {
-    const uint32_t ub = D.g0 + 16u * u;  // the unit's first block
-    if (ub >= D.g1) break;
-    if ((lane >> 4) == u) {
-      uint4* img = reinterpret_cast<uint4*>(tile + (lane & 15u) * xf::kTile);
+  for (uint32_t u = 0; 16u * u < nrest; u++) {
+    // the unit's blocks: compacted positions 16u .. 16u+15 (slots past the
+    // last block are zero, so they do not keep steps alive)
+    const bool mine = D.live && !isdc && (rrank >> 4) == u;
+    if (mine) {
+      uint4* img = reinterpret_cast<uint4*>(tile + (rrank & 15u) * xf::kTile);
 #pragma unroll
       for (int c = 0; c < 8; c++) img[c] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
+    } else if (lane < 16u && 16u * u + lane >= nrest) {
+      uint4* img = reinterpret_cast<uint4*>(tile + lane * xf::kTile);
+#pragma unroll
+      for (int c = 0; c < 8; c++) img[c] = make_uint4(0u, 0u, 0u, 0u);
     }
     xf::wave_sync();
     uint2 w0, w1;
     xf::idct_rows(tile + b * xf::kTile, q, sq, w0, w1);
-    if (ub + b < D.g1) {
-      const uint32_t off = xf::block_row_offset(U, ub + b - U.cum, 2u * q);
+    if (16u * u + b < nrest) {
+      const uint32_t gl = D.g0 + s_blk[16u * u + b];  // the block of compacted position 16u + b
+      const uint32_t off = xf::block_row_offset(U, gl - U.cum, 2u * q);
       *reinterpret_cast<uint2*>(fr + off) = w0;
       *reinterpret_cast<uint2*>(fr + off + U.pw) = w1;
     }
