@@ -131,6 +131,10 @@ __global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ 
   }
 }
 
+struct alignas(4) Dw4 {  // a 16-byte store at a dword-aligned address (global_store_dwordx4)
+  uint32_t x, y, z, w;
+};
+
 __device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uint32_t* tile_pre,
                                             uint32_t g) {
   return local_off[g] + tile_pre[g / kScanTile];
@@ -295,7 +299,20 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
     for (uint32_t k = 0; k < lead; k++) out[P + k] = (uint8_t)(w >> (8 * k));
   }
   uint32_t j0 = 0;  // first source word held in v
-  for (uint32_t k = lead; k < sz; k += 4) {
+  uint32_t k = lead;
+  // 16 chunk bytes per store while 16 remain (the wave's loop runs to its
+  // longest chunk: a quarter of the iterations of dword stores)
+  for (; k + 16u <= sz; k += 16u) {
+    const uint32_t need = (sh + k) >> 2;
+    if (need + 4 >= j0 + 9) {  // refill
+      j0 = need;
+#pragma unroll
+      for (uint32_t i = 0; i < 9; i++) v[i] = (j0 + i < nsrc) ? src[j0 + i] : 0u;
+    }
+    const Dw4 o{word_at(k, v, j0), word_at(k + 4, v, j0), word_at(k + 8, v, j0), word_at(k + 12, v, j0)};
+    *reinterpret_cast<Dw4*>(out + P + k) = o;  // (4-byte aligned: P + lead is)
+  }
+  for (; k < sz; k += 4) {
     const uint32_t need = (sh + k) >> 2;
     if (need + 1 >= j0 + 9) {  // refill (chunks over ~28 bytes)
       j0 = need;
