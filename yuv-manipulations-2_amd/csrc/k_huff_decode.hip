@@ -44,6 +44,10 @@ namespace {
 // 6 KiB stage: 96 B of chunk per block on average (a 4K frame at q=50 uses
 // ~12 B); a wave whose chunks do not fit is staged in several rounds.
 constexpr uint32_t kStageQuads = 384;
+// One zero quad after the stage (zeroed at kernel start, never staged into):
+// the symbol loop reads a lane's value from it when the lane takes none, so
+// the value needs no select.
+constexpr uint32_t kZeroBit = kStageQuads * 128u;
 
 // diagnostic ablations (never the product): 1 = no symbol decode, 2 = no
 // table parse either, 3 = the fused decoder skips its transform
@@ -206,9 +210,9 @@ __device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T
     // the value: 16-bit field n of gpos (a 64-bit shift uses its count mod 64)
     const uint32_t G = (uint32_t)((n < 4 ? glo : ghi) >> (n << 4)) & 0xFFFFu;
     const uint32_t vbit = (w8 >> ((7 - n) & 7)) * 11u + G + vbase;
-    const uint32_t P = take ? vbit : 0u, w = P >> 5;
+    const uint32_t P = take ? vbit : kZeroBit, w = P >> 5;  // (stage bits; kZeroBit: the zero quad)
     const uint32_t raw = funnel(c.st[w + 1], c.st[w], P);
-    const uint32_t v = take ? (uint32_t)(((int32_t)(raw << 21)) >> 21) : 0u;
+    const uint32_t v = (uint32_t)(((int32_t)(raw << 21)) >> 21);
     const int z = c_zz[j];
     if (z & 1) nw[z >> 1] |= v << 16;
     else nw[z >> 1] |= v & 0xFFFFu;
@@ -435,7 +439,8 @@ __global__ __launch_bounds__(64, MYYUV_K5S_WAVES) void k_huff_decode(const uint8
                                                    uint4* __restrict__ coef,
                                                    uint8_t* __restrict__ rmask,
                                                    unsigned long long* __restrict__ err) {
-  __shared__ uint4 stq[kStageQuads];
+  __shared__ uint4 stq[kStageQuads + 1];
+  if (threadIdx.x == 0) stq[kStageQuads] = make_uint4(0u, 0u, 0u, 0u);  // (ordered by decode_group's barrier)
   if (desc[blockIdx.y].bad) return;
   DecodeGroup D;
   uint32_t nw[32];
@@ -486,10 +491,11 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
                                                    uint8_t* __restrict__ frame,
                                                    unsigned long long* __restrict__ err) {
   static_assert(sizeof(uint4) * kStageQuads >= sizeof(float) * xf::kXfTile16, "the tile over the stage");
-  __shared__ uint4 stq[kStageQuads];
+  __shared__ uint4 stq[kStageQuads + 1];
   __shared__ float sq[64];
   __shared__ uint16_t s_blk[64];
   const uint32_t lane = threadIdx.x;
+  if (lane == 0) stq[kStageQuads] = make_uint4(0u, 0u, 0u, 0u);  // (ordered by decode_group's barrier)
   {
     const uint32_t t = blockIdx.x;
     const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
