@@ -2,7 +2,8 @@
 """Diagnostic: per-kernel times of one 7-frame launch group (chef-big q50,
 batch entry points, kernels alone on the GPU, HIP events, no correctness
 checks) for the library builds given as arguments (directories holding a
-libmyyuv_hip.so, or "default"), three alternating rounds:
+libmyyuv_hip.so, "default", or VAR=value: the in-tree build with that
+environment), three alternating rounds:
   python3 tools/k1_ab.py default build_var/x ..."""
 import os
 import subprocess
@@ -46,7 +47,10 @@ def main():
     for rnd in range(3):
         for lib in libs:
             env = dict(os.environ)
-            if lib != "default":
+            if "=" in lib:
+                k, v = lib.split("=", 1)
+                env[k] = v
+            elif lib != "default":
                 env["MYYUV_HIP_LIB"] = os.path.join(ROOT, lib, "libmyyuv_hip.so")
             r = subprocess.run([sys.executable, "-c", CHILD % (ROOT, PKG, ROOT)], env=env, capture_output=True,
                                text=True, timeout=300)

@@ -1,0 +1,12 @@
+# span decoder (k_decode_span: 256-block spans, DC-only chunks straight from the stream, rest blocks
+# in size-bucketed rounds) against the 64-block fused decoder (MYYUV_DECODER=wave); 4 vs 5 waves/SIMD
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3zs_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r3zs_tests.log; exit 1; }
+tail -1 gpurun_out/r3zs_tests.log
+timeout -k 10 300 python3 tools/k1_ab.py MYYUV_DECODER=wave default build_var/span5 > gpurun_out/r3zs_kernels.txt 2>&1 || { echo KAB_FAILED; tail -20 gpurun_out/r3zs_kernels.txt; exit 1; }
+cat gpurun_out/r3zs_kernels.txt
+timeout -k 10 500 bash tools/ab_bench.sh MYYUV_DECODER=wave default build_var/span5 > gpurun_out/r3zs_ab.txt 2>&1 || { echo AB_FAILED; tail -20 gpurun_out/r3zs_ab.txt; exit 1; }
+cp gpurun_out/ab_bench.txt gpurun_out/r3zs_ab.txt
+cat gpurun_out/r3zs_ab.txt
