@@ -332,8 +332,16 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   const uint32_t csize = desc->content_size[p];
   const uint32_t E = cpos + min(end_scan - plane_pre, csize);
   const uint32_t gl = live ? g : g1 - 1;
-  const uint32_t rel = scanned(local_off, tile_pre, gl) - plane_pre;
   const uint32_t s = in[desc->sizes_pos[p] + (gl - G.cum[p])];
+  // the chunk's offset: the group's (k_scan_chain keeps group starts only)
+  // plus the wave's exclusive scan of the sizes
+  uint32_t incl = live ? s : 0u;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  const uint32_t rel = scanned(local_off, tile_pre, g0) - plane_pre + incl - (live ? s : 0u);
 
   // plane-level check (DCT.cpp:21-33 reads past content_size otherwise):
   // the chunks must fit the declared content.

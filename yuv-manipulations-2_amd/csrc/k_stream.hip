@@ -47,7 +47,9 @@ __device__ __forceinline__ int plane_of(const uint32_t cum[4], uint32_t g) {
 // its bytes at src + blockIdx.y * src_stride): workgroup t scans tile t
 // (kScanTile sizes) and finds the tile's exclusive prefix by decoupled
 // look-back over the lower tiles (k_chain.hpp); local_off[g] = offset inside
-// the tile, tile_pre[t] = the tile's prefix, tile_pre[ntiles] = the total.
+// the tile, written only where a decoder wave's 64-block group starts (g -
+// cum[p] a multiple of 64: the decoders scan their own 64 sizes from there),
+// tile_pre[t] = the tile's prefix, tile_pre[ntiles] = the total.
 // Element g's size byte is src[pos[p] + (g - cum[p])].  With `desc` (decode)
 // every workgroup first parses the stream header (k_parse's checks, DCTYUV::load
 // DCT.cpp:130-159 then DCTYUVPlane::load :39-62) for the size positions, and
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ 
   }
   const uint32_t base = blockIdx.x * kScanTile + threadIdx.x * kScanPerThread;
   uint32_t v[kScanPerThread];
-  uint32_t sum = 0;
+  uint32_t sum = 0, lead = 0;  // lead bit i: element i starts a decode group
 #pragma unroll
   for (int i = 0; i < kScanPerThread; i++) {
     const uint32_t g = base + i;
@@ -102,6 +104,7 @@ __global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ 
     if (g < S.cum[3]) {
       const int p = plane_of(S.cum, g);
       s = src[pos[p] + (g - S.cum[p])];
+      lead |= (((g - S.cum[p]) & (kWave - 1)) == 0 ? 1u : 0u) << i;
     }
     v[i] = s;
     sum += s;
@@ -120,8 +123,7 @@ __global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ 
   uint32_t run = carry + incl - sum;
 #pragma unroll
   for (int i = 0; i < kScanPerThread; i++) {
-    const uint32_t g = base + i;
-    if (g < S.cum[3]) local_off[g] = run;
+    if ((lead >> i) & 1u) local_off[base + i] = run;  // the decoders read group starts only
     run += v[i];
   }
   __syncthreads();
