@@ -173,7 +173,7 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
 #define MYYUV_K_HUFF_DEC 5   /* K5 huff_decode */
 #define MYYUV_K_IDCT 6       /* K6 dequant_idct */
 #define MYYUV_K_HUFF_WIDE 7  /* K2 overflow pass, lane per block (long worklists) */
-#define MYYUV_K_SCAN_SUMS 8  /* (unused: the scan is single-pass) */
+#define MYYUV_K_HUFF_R16 8   /* K2 overflow tier 1: register-resident, up to 16 symbols, lane per block */
 #define MYYUV_K_HUFF_WAVE 9  /* K2 overflow pass, wave per block (short worklists) */
 #define MYYUV_K_BMP 10       /* K7 bmp_to_iyuv (BMP -> IYUV conversion) */
 #define MYYUV_K_COUNT 11

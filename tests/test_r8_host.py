@@ -126,3 +126,78 @@ def test_dense_run_matches_concatenated_chunks(harness, oracle):
             want += bytes(oracle.huff_encode_block(x))
     assert total == len(want)
     assert out[4:] == want
+
+
+def check16(exe, oracle, nat):
+    """The CAP-16 tier (huff_r16.hpp build_r16 + emit_chunk16): the oracle's
+    chunk for every block with at most 16 distinct symbols, declined above."""
+    nat = np.asarray(nat, np.int16).reshape(-1, 64)
+    got = run(exe, nat, "16")
+    n_ok = 0
+    for x, ch in zip(nat, got):
+        msg = x[ZZ]
+        nz = np.nonzero(msg)[0]
+        m = nz[-1] + 1 if len(nz) else 1
+        if len(set(msg[:m].tolist())) > 16:
+            assert ch is None
+            continue
+        assert ch == bytes(oracle.huff_encode_block(x)), msg[:m]
+        n_ok += 1
+    return n_ok
+
+
+def test_r16_rehash_boundaries(harness, oracle):
+    """12..16 distinct symbols, with and without a zero inside the message,
+    with and without trailing zeros: the map's rehash to 29 buckets before
+    the 14th key, or before the freq[0] probe inserts key 0 into a 13-key map
+    (Huffman.cpp:186-197), and the libstdc++ heap over up to 16 entries."""
+    rng = np.random.default_rng(16)
+    nat = []
+    for k in range(12, 17):
+        for zero in (False, True):
+            for full in (False, True):
+                for _ in range(150):
+                    m = 64 if full else int(rng.integers(k + 2, 64))
+                    vals = rng.choice(np.arange(1, 60), size=k, replace=False) * rng.choice([-1, 1], size=k)
+                    if zero:
+                        vals[0] = 0
+                    msg = rng.choice(vals, size=m)
+                    msg[:k] = vals
+                    rng.shuffle(msg)
+                    if msg[-1] == 0:
+                        j = np.nonzero(msg)[0][-1]
+                        msg[-1], msg[j] = msg[j], msg[-1]
+                    x = np.zeros(64, np.int16)
+                    x[ZZ[:m]] = msg
+                    nat.append(x)
+    assert check16(harness, oracle, nat) == len(nat)
+
+
+def test_r16_random_and_edge_blocks(harness, oracle):
+    rng = np.random.default_rng(17)
+    nat = np.zeros((6000, 64), np.int16)
+    for x in nat:
+        m = rng.integers(1, 65)
+        msg = rng.integers(-8, 9, size=m)
+        if msg[-1] == 0:
+            msg[-1] = 1
+        x[ZZ[:m]] = msg
+    edge = []
+    for _, b in blockgen.edge_blocks():
+        x = np.zeros(64, np.int16)
+        x[ZZ] = b
+        edge.append(x)
+    assert check16(harness, oracle, np.concatenate([nat, np.array(edge)])) > 4000
+
+
+def test_r16_golden_frame_blocks(harness, oracle, golden):
+    f = golden("chef-with-trumpet-big-DCT-50.myyuv")
+    raw = np.frombuffer(oracle.decompress(f.data, f.width, f.height, tuple(f.params)), np.uint8)
+    w, h = f.width, f.height
+    y = raw[:w * h].reshape(h // 8, 8, w // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64)
+    rng = np.random.default_rng(3)
+    pick = rng.choice(len(y), 2000, replace=False)
+    for q in (50, 90, 100):
+        Q = oracle.qtable(q, 0)
+        nat = np.stack([oracle.fdct_block(y[i], Q) for i in pick])
+        assert check16(harness, oracle, nat) > 1900

@@ -60,7 +60,7 @@ torch.cuda.synchronize()
 base = max(run(0), run(0))
 print(f"all kernels: {base:9.0f} MP/s")
 for kid, name in enumerate(myyuv_hip.KERNELS):
-    if name in ("parse", "scan_sums"):
+    if name in ("parse",):
         continue
     v = max(run(1 << kid), run(1 << kid))
     print(f"skip {name:16s}: {v:9.0f} MP/s  ({(1 / base - 1 / v) * B * w * h / 1e6 * 1e6 / B:7.1f} us/frame)")

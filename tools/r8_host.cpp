@@ -3,7 +3,8 @@
 // writes the chunks to stdout, for tests/test_r8_host.py to compare with the
 // oracle.  argv[1]: "4" / "8" = build_r<CAP> + emit_chunk on every block;
 // "auto" = the kernel's class dispatch (block_class); "dense" = "auto" packed
-// the way k_huff_encode packs a tile (DenseWriter).
+// the way k_huff_encode packs a tile (DenseWriter); "16" = build_r16 +
+// emit_chunk16 (the CAP-16 overflow tier, huff_r16.hpp).
 //   in:  u32 n, then n x 64 int16 coefficients in natural order
 //   out: per block u8 ok, u8 size, then `size` chunk bytes (ok = 1);
 //        "dense": u32 run bytes, then the run
@@ -12,6 +13,7 @@
 #include <vector>
 
 #include "huff_common.hpp"
+#include "huff_r16.hpp"
 
 using namespace myyuv_gpu;
 
@@ -60,6 +62,26 @@ int main(int argc, char** argv) {
     for (int w = 0; w < 32; w++)
       R.w[w] = (uint16_t)c[b * 64 + 2 * w] | ((uint32_t)(uint16_t)c[b * 64 + 2 * w + 1] << 16);
     ok[b] = build(R, mode[0] == 'd' ? "auto" : mode, st[b]);
+  }
+  if (mode[0] == '1') {  // "16": the CAP-16 tier
+    for (uint32_t b = 0; b < n; b++) {
+      CoefRegs R;
+      for (int w = 0; w < 32; w++)
+        R.w[w] = (uint16_t)c[b * 64 + 2 * w] | ((uint32_t)(uint16_t)c[b * 64 + 2 * w + 1] << 16);
+      EncState16 S16;
+      const bool ok16 = build_r16(R, R.msz(), 64, S16);
+      const uint8_t hdr[2] = {(uint8_t)ok16, ok16 ? (uint8_t)S16.size : (uint8_t)0};
+      fwrite(hdr, 1, 2, stdout);
+      if (ok16) {
+        uint8_t bytes[kMaxChunk] = {0};
+        HostWriter hw{bytes};
+        emit_chunk16(S16, 64, hw);
+        hw.align_byte();
+        if (hw.pos != (int)S16.size) return 3;
+        fwrite(bytes, 1, S16.size, stdout);
+      }
+    }
+    return 0;
   }
   if (mode[0] == 'd') {
     // "dense": K2's tile run — the accepted blocks' chunks back to back in

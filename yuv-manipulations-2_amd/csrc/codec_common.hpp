@@ -122,6 +122,17 @@ constexpr uint32_t kWideLanes = MYYUV_WIDE_LANES;  // blocks (lanes) per workgro
 #define MYYUV_WIDE_GRID (1280 * 64 / MYYUV_WIDE_LANES)
 #endif
 constexpr uint32_t kWideGrid = MYYUV_WIDE_GRID;  // workgroups of k_huff_encode_wide: its LDS fits 5 x 64 lanes per CU
+// Overflow lists longer than one resident round of k_huff_encode_wide (its
+// grid x lanes) go through the CAP-16 register tier first
+// (k_huff_encode_r16, huff_r16.hpp); it lists the blocks with more than 16
+// distinct symbols again (work2) for the wave / lane passes.  Shorter lists
+// (every launch group of the bench) skip it: there one CAP-64 round takes the
+// whole list, and the extra pass measured slower (profiles/r3g_*).
+#ifndef MYYUV_R16_GATE
+#define MYYUV_R16_GATE (MYYUV_WIDE_GRID * MYYUV_WIDE_LANES)
+#endif
+constexpr uint32_t kR16Gate = MYYUV_R16_GATE;
+constexpr uint32_t kR16Grid = 4096;  // workgroups of k_huff_encode_r16 (grid-stride, 64 blocks each)
 #ifndef MYYUV_K2_GROUP
 #define MYYUV_K2_GROUP 256
 #endif

@@ -60,6 +60,7 @@ extern __device__ uint32_t g_k2_fstamps[8192 * 8];
   } while (0)
 #endif
 #include "huff_common.hpp"
+#include "huff_r16.hpp"
 #include "xform_common.hpp"
 
 namespace myyuv_gpu {
@@ -722,6 +723,21 @@ __device__ void encode_block_wave(const uint4* __restrict__ coef, const uint8_t*
 
 }  // namespace
 
+// The list the wave / lane overflow passes take: K2's (`work`), or, when it
+// is longer than `gate` (kR16Gate when k_huff_encode_r16 ran, else ~0u), what
+// the CAP-16 tier left (`work2`).
+struct OvfList {
+  const uint32_t* ids;
+  uint32_t n;
+};
+__device__ __forceinline__ OvfList overflow_list(const uint32_t* work, const uint32_t* work_count,
+                                                 const uint32_t* work2, const uint32_t* work2_count,
+                                                 uint32_t gate) {
+  const uint32_t cnt = *work_count;
+  if (cnt <= gate) return OvfList{work, cnt};
+  return OvfList{work2, *work2_count};
+}
+
 // Overflow pass for short worklists: one wave per listed block (see
 // encode_block_wave); exits at once when the list is long (the lane pass
 // k_huff_encode_wide takes it).
@@ -732,12 +748,15 @@ __global__ __launch_bounds__(64) void k_huff_encode_wave(const uint4* __restrict
                                                         uint32_t* __restrict__ tinfo,
                                                         const uint32_t* __restrict__ work,
                                                         const uint32_t* __restrict__ work_count,
-                                                        uint32_t limit) {
+                                                        const uint32_t* __restrict__ work2,
+                                                        const uint32_t* __restrict__ work2_count,
+                                                        uint32_t gate, uint32_t limit) {
   __shared__ uint32_t img[kSlotWords + 2];
-  const uint32_t cnt = *work_count;
+  const OvfList L = overflow_list(work, work_count, work2, work2_count, gate);
+  const uint32_t cnt = L.n;
   if (cnt > limit) return;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-    const uint32_t g = work[i];
+    const uint32_t g = L.ids[i];
     encode_block_wave(coef, rmask, g, img, oslots, sizes, tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, i);
   }
 }
@@ -1337,8 +1356,9 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
 
 // Overflow pass (CAP=64), lane per block, for long worklists (noise-like
 // frames where most blocks overflow): the blocks listed in `work` (count in
-// *work_count), 64 per workgroup; the grid is sized for the worst case, idle
-// groups exit.  Lists of at most `limit` blocks go to k_huff_encode_wave instead.
+// *work_count; past kR16Gate what the CAP-16 tier left in `work2`), 64 per
+// workgroup; the grid is sized for the worst case, idle groups exit.  Lists
+// of at most `limit` blocks go to k_huff_encode_wave instead.
 __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __restrict__ coef,
                                                         const uint8_t* __restrict__ rmask,
                                                         const uint4* __restrict__ zq, FrameGeom G,
@@ -1347,17 +1367,20 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
                                                         uint32_t* __restrict__ tinfo,
                                                         const uint32_t* __restrict__ work,
                                                         const uint32_t* __restrict__ work_count,
-                                                        uint32_t limit) {
+                                                        const uint32_t* __restrict__ work2,
+                                                        const uint32_t* __restrict__ work2_count,
+                                                        uint32_t gate, uint32_t limit) {
   constexpr int CAP = 64;
   __shared__ uint32_t lds[Layout<CAP>::kWords * kWideLanes];
-  const uint32_t cnt = *work_count;
+  const OvfList L = overflow_list(work, work_count, work2, work2_count, gate);
+  const uint32_t cnt = L.n;
   if (cnt <= limit) return;  // short lists: k_huff_encode_wave
   // grid-stride over kWideLanes-block slices of the list (the grid is what
   // the 512 B-per-lane LDS lets be resident)
   for (uint32_t base = blockIdx.x * kWideLanes; base < cnt; base += gridDim.x * kWideLanes) {
     const uint32_t i = base + threadIdx.x;
     const bool live = i < cnt;
-    const uint32_t g = live ? work[i] : 0;
+    const uint32_t g = live ? L.ids[i] : 0;
     CoefRegs R;
     R.load(coef, zq, g, live ? rmask[g] : 0u);
     const int msz = live ? R.msz() : 0;
@@ -1366,6 +1389,57 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
       const Img<CAP> I{lds, (int)threadIdx.x};
       encode_block<CAP>(I, R, msz, max(wmsz, 1), oslots + (size_t)g * kSlotWords, sizes + g);
       atomicAdd(tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, (uint32_t)sizes[g]);  // (this lane's own store)
+    }
+  }
+}
+
+// Overflow tier 1 for long lists (more than kR16Gate blocks, i.e. more than
+// one resident round of k_huff_encode_wide): register-resident, CAP 16
+// (huff_r16.hpp), lane per block, 64 blocks per workgroup, grid-stride;
+// blocks with more than 16 distinct symbols go on to `work2` for the wave /
+// lane passes.  Natural images put nearly all overflow blocks here (q50:
+// 99.8 %, q90: 94 %), so past one CAP-64 round the list costs one lane's
+// register program per block instead of the LDS replay's chain of dependent
+// round trips (8192^2 q90: 214 -> 145 us with the wave pass on work2,
+// profiles/r3t_*).
+__global__ __launch_bounds__(64) void k_huff_encode_r16(const uint4* __restrict__ coef,
+                                                        const uint8_t* __restrict__ rmask,
+                                                        const uint4* __restrict__ zq, FrameGeom G,
+                                                        uint32_t* __restrict__ oslots,
+                                                        uint8_t* __restrict__ sizes,
+                                                        uint32_t* __restrict__ tinfo,
+                                                        const uint32_t* __restrict__ work,
+                                                        const uint32_t* __restrict__ work_count,
+                                                        uint32_t* __restrict__ work2,
+                                                        uint32_t* __restrict__ work2_count) {
+  const uint32_t cnt = *work_count;
+  if (cnt <= kR16Gate) return;  // one CAP-64 round takes the list
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t base = blockIdx.x * kWave; base < cnt; base += gridDim.x * kWave) {
+    const uint32_t i = base + lane;
+    const bool live = i < cnt;
+    const uint32_t g = live ? work[i] : 0u;
+    CoefRegs R;
+    R.load(coef, zq, g, live ? rmask[g] : 0u);
+    const int msz = live ? R.msz() : 0;
+    const int wmsz = max(wave_max(msz), 1);
+    EncState16 S;
+    const bool ok = live && build_r16(R, msz, wmsz, S);
+    if (ok) {
+      BitWriter bw;
+      bw.out = oslots + (size_t)g * kSlotWords;
+      emit_chunk16(S, wmsz, bw);
+      bw.align_byte();
+      bw.flush();
+      sizes[g] = (uint8_t)S.size;
+      atomicAdd(tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, S.size);  // the tile's overflow bytes
+    }
+    const uint64_t more = __ballot(live && !ok);
+    if (more) {
+      uint32_t b0 = 0;
+      if (lane == 0) b0 = atomicAdd(work2_count, (uint32_t)__popcll(more));
+      b0 = __builtin_amdgcn_readfirstlane(b0);
+      if ((more >> lane) & 1ull) work2[b0 + (uint32_t)__popcll(more & ((1ull << lane) - 1ull))] = g;
     }
   }
 }

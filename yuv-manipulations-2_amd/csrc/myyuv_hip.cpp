@@ -32,9 +32,13 @@ __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const S
 __global__ void k_huff_encode(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
                               uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
-                                   const uint32_t*, const uint32_t*, uint32_t);
+                                   const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t,
+                                   uint32_t);
 __global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
-                                   uint32_t*, const uint32_t*, const uint32_t*, uint32_t);
+                                   uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                                   uint32_t, uint32_t);
+__global__ void k_huff_encode_r16(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
+                                  uint32_t*, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_encode_tile(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint32_t*, uint32_t*,
                               uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_tile_scan(uint32_t*, FrameGeom, uint8_t*, uint32_t, uint32_t*, unsigned long long*);
@@ -327,7 +331,8 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->sink.grow(192 * 16);  // K1/K6: 2 x 64 quads + K1's 64 mask bytes
   e |= c->psize.grow(4);
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
-  e |= c->work.grow((size_t)nblk * 4 + 256);  // [0]: overflow count, then block ids
+  // [0], [1]: overflow counts, then K2's list and (single frames) the CAP-16 tier's (launch_overflow)
+  e |= c->work.grow((size_t)nblk * (nf == 1 ? 8 : 4) + 256);
   const size_t st_bytes = (size_t)nf * (ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
@@ -351,6 +356,11 @@ uint32_t next_epoch(myyuv_hip_ctx* c) {
 // returns at once outside its regime.  A batch (nf > 1) takes the
 // lane-per-block pass only: its list is long, and the wave pass's per-block
 // SALU cost would crowd the other launch groups in flight (tools/kskip.py).
+// A single frame's list longer than one resident round of the lane pass
+// (kR16Gate) goes through the CAP-16 register tier first (k_huff_encode_r16),
+// and the two passes then take what it leaves (more than 16 symbols: work[1]
+// blocks from word 64 + nblk).  work[0] is zeroed by K1 (or the host),
+// work[1] here.
 int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s);
 
 int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
@@ -369,18 +379,33 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   const uint32_t nf = G.nframes, nblk = G.cum[3] * nf;
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
+  uint32_t* count2 = count + 1;
+  uint32_t* list2 = list + nblk;
   const uint32_t limit = nf > 1 ? kBatchWaveLimit : kWaveEncodeLimit;
   int e = 0;
+  const uint32_t gate = nf == 1 && nblk > kR16Gate ? kR16Gate : ~0u;
+  // (batches keep the CAP-64 pass alone: the tier's launch in every launch
+  // group cost 3.4 % of the bench, profiles/r3zw_*)
+  if (gate != ~0u) {
+    // work[1], the tier's count (its own node: a store in K1's prologue
+    // shifted K1's loop and cost it 5 %, profiles/r3zx_*)
+    e |= hipMemsetAsync(count2, 0, 4, s) != hipSuccess;
+    const uint32_t r16 = ceil_div(nblk, kWave) < kR16Grid ? ceil_div(nblk, kWave) : kR16Grid;
+    e |= launch(c, MYYUV_K_HUFF_R16, k_huff_encode_r16, dim3(r16), dim3(kWave), s, c->coef.as<const uint4>(),
+                c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G, c->oslots.as<uint32_t>(),
+                c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
+                list2, count2);
+  }
   if (limit > 0)
     e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
                 c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), G, c->oslots.as<uint32_t>(),
                 c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
-                limit);
+                (const uint32_t*)list2, (const uint32_t*)count2, gate, limit);
   const uint32_t wide = ceil_div(nblk, kWideLanes) < kWideGrid ? ceil_div(nblk, kWideLanes) : kWideGrid;
   e |= launch(c, MYYUV_K_HUFF_WIDE, k_huff_encode_wide, dim3(wide), dim3(kWideLanes), s,
               c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
               c->oslots.as<uint32_t>(), c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list,
-              (const uint32_t*)count, limit);
+              (const uint32_t*)count, (const uint32_t*)list2, (const uint32_t*)count2, gate, limit);
   return e;
 }
 
