@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PEAK_GBS = 8000.0
 W = H = 8192
 SAMPLES = W * H * 3 // 2
-ENC = ("fdct_quant", "huff_encode", "huff_encode_wave", "huff_encode_wide", "tile_scan", "stream_out")
+ENC = ("fdct_quant", "huff_encode", "huff_encode_r16", "huff_encode_wave", "huff_encode_wide", "tile_scan", "stream_out")
 DEC = ("scan_chain", "decode_idct")
 
 
