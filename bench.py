@@ -5,7 +5,7 @@ Workloads (--workload; `auto`, the default, picks chef-big at one rank and
 batch4k at more):
   chef-big  BASELINE.json configs[1], the metric's own configuration: a step
             is one DCT compress + decompress round trip of --inflight x
-            --batch (default 3 x 16 = 48) 4032x3008 IYUV frames per rank
+            --batch (default 3 x 24 = 72) 4032x3008 IYUV frames per rank
             (chef-with-trumpet-big, q=50; its raw input is missing from the
             reference, so the frame is the sha-pinned decode of
             chef-with-trumpet-big-DCT-50.myyuv), read from --input-frames
@@ -134,10 +134,9 @@ def parse(argv=None):
                     help="time the step without K1's HIP events (no roofline)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="launch groups in flight per GPU, each on its own codec context and HIP stream "
-                         "(1 = strictly serial; 0 = the workload's default: chef-big 3, batch4k 4)")
+                         "(1 = strictly serial; 0 = 3)")
     ap.add_argument("--batch", type=int, default=0,
-                    help="frames per launch (the batch entry points; 0 = the workload's default: chef-big 16, "
-                         "batch4k 8)")
+                    help="frames per launch (the batch entry points; 0 = 24)")
     ap.add_argument("--stream-priority", default="",
                     help="comma-separated HIP stream priorities of the launch groups' streams "
                          "(cycled; default all normal)")
@@ -152,7 +151,7 @@ def parse(argv=None):
     ap.add_argument("--input-frames", type=int, default=0,
                     help="chef-big: distinct HBM copies of the input frame the launch groups read in turn "
                          "(0: one per frame of a step, at least 24; rounded down to a multiple of --batch: "
-                         "48 copies, 873 MB at the default 3 x 16, larger than the 256 MiB Infinity Cache)")
+                         "72 copies, 1.31 GB at the default 3 x 24, larger than the 256 MiB Infinity Cache)")
     ap.add_argument("--cpu-codec", action="store_true",
                     help="tests only: the CPU restatement as the codec, host tensors, gloo (no GPU)")
     ap.add_argument("--launch-selftest", action="store_true",
@@ -486,7 +485,7 @@ class Run:
         self.verified = {}
         if name == "chef-big":
             self.w, self.h = big.width, big.height
-            self.B = args.batch or 16
+            self.B = args.batch or 24
             self.per_step = self.nf * self.B
             self.n_local = self.per_step
             self.n_total = world * self.per_step
@@ -508,7 +507,7 @@ class Run:
             if self.n_total < world or self.n_total % world or self.n_total > man["frames_total"]:
                 raise SystemExit(f"--frames {self.n_total}: a multiple of the {world} ranks, at most "
                                  f"{man['frames_total']}")
-            self.B = args.batch or 8
+            self.B = args.batch or 24
             self.n_local = self.n_total // world
             self.per_step = self.n_local
             self.cap = SLOT_4K
@@ -780,9 +779,10 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     name = args.workload if args.workload != "auto" else ("chef-big" if world == 1 else "batch4k")
     dist = None
-    # launch shape: chef-big 3 x 16 (driver shape 240.8k against 236.7k MP/s for 4 x 8, three rounds,
-    # profiles/r3zzc_launch_shape.txt), batch4k 4 x 8
-    nf = max(1, args.inflight or (3 if name == "chef-big" else 4))
+    # launch shape 3 x 24: the launch groups' overflow lists (~200k blocks) take the CAP-16 tier;
+    # chef-big driver shape 264.2k against 233.1k MP/s for 4 x 8 (two rounds, profiles/r3zzf_*, r3zzg_*,
+    # flat from 3 x 24 to 3 x 48), batch4k 263.0k against 243.3k (profiles/r3zzh_*)
+    nf = max(1, args.inflight or 3)
     prios = [int(v) for v in args.stream_priority.split(",")] if args.stream_priority else [0]
     big = myyuv_file.YUVFile.load(GOLDEN_BIG)
     if args.cpu_codec:

@@ -126,8 +126,8 @@ constexpr uint32_t kWideGrid = MYYUV_WIDE_GRID;  // workgroups of k_huff_encode_
 // grid x lanes) go through the CAP-16 register tier first
 // (k_huff_encode_r16, huff_r16.hpp); it lists the blocks with more than 16
 // distinct symbols again (work2) for the wave / lane passes.  Shorter lists
-// (every launch group of the bench) skip it: there one CAP-64 round takes the
-// whole list, and the extra pass measured slower (profiles/r3g_*).
+// skip it: one CAP-64 round takes the whole list, and there the extra pass
+// measured slower (profiles/r3g_*).
 #ifndef MYYUV_R16_GATE
 #define MYYUV_R16_GATE (MYYUV_WIDE_GRID * MYYUV_WIDE_LANES)
 #endif

@@ -22,6 +22,10 @@
 #include "k_stream.hpp"
 #include "myyuv_hip.h"
 
+#ifndef MYYUV_R16_BATCH
+#define MYYUV_R16_BATCH 1  // batches take the CAP-16 overflow tier too (0: single frames only)
+#endif
+
 namespace myyuv_gpu {
 __global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*);
 __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*,
@@ -332,7 +336,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->psize.grow(4);
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
   // [0], [1]: overflow counts, then K2's list and (single frames) the CAP-16 tier's (launch_overflow)
-  e |= c->work.grow((size_t)nblk * (nf == 1 ? 8 : 4) + 256);
+  e |= c->work.grow((size_t)nblk * (nf == 1 || MYYUV_R16_BATCH ? 8 : 4) + 256);
   const size_t st_bytes = (size_t)nf * (ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
@@ -356,11 +360,10 @@ uint32_t next_epoch(myyuv_hip_ctx* c) {
 // returns at once outside its regime.  A batch (nf > 1) takes the
 // lane-per-block pass only: its list is long, and the wave pass's per-block
 // SALU cost would crowd the other launch groups in flight (tools/kskip.py).
-// A single frame's list longer than one resident round of the lane pass
-// (kR16Gate) goes through the CAP-16 register tier first (k_huff_encode_r16),
-// and the two passes then take what it leaves (more than 16 symbols: work[1]
-// blocks from word 64 + nblk).  work[0] is zeroed by K1 (or the host),
-// work[1] here.
+// A list longer than one resident round of the lane pass (kR16Gate) goes
+// through the CAP-16 register tier first (k_huff_encode_r16), and the two
+// passes then take what it leaves (more than 16 symbols: work[1] blocks from
+// word 64 + nblk).  work[0] is zeroed by K1 (or the host), work[1] here.
 int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s);
 
 int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
@@ -383,9 +386,10 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   uint32_t* list2 = list + nblk;
   const uint32_t limit = nf > 1 ? kBatchWaveLimit : kWaveEncodeLimit;
   int e = 0;
-  const uint32_t gate = nf == 1 && nblk > kR16Gate ? kR16Gate : ~0u;
-  // (batches keep the CAP-64 pass alone: the tier's launch in every launch
-  // group cost 3.4 % of the bench, profiles/r3zw_*)
+  const uint32_t gate = (nf == 1 || MYYUV_R16_BATCH) && nblk > kR16Gate ? kR16Gate : ~0u;
+  // (launched whenever such a list is possible; with 8-frame launch groups,
+  // whose lists stay below the gate, the empty launch cost 3.4 % of the
+  // bench, profiles/r3zw_*; the bench's 24-frame groups take the tier)
   if (gate != ~0u) {
     // work[1], the tier's count (its own node: a store in K1's prologue
     // shifted K1's loop and cost it 5 %, profiles/r3zx_*)
