@@ -1402,7 +1402,10 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
 // register program per block instead of the LDS replay's chain of dependent
 // round trips (8192^2 q90: 214 -> 145 us with the wave pass on work2,
 // profiles/r3t_*).
-__global__ __launch_bounds__(64) void k_huff_encode_r16(const uint4* __restrict__ coef,
+#ifndef MYYUV_R16_WAVES
+#define MYYUV_R16_WAVES 5  // waves per SIMD k_huff_encode_r16 is compiled for: 96 VGPRs, 8 spilled (3 waves at 131: -1.5 %, profiles/r3zzl_*)
+#endif
+__global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const uint4* __restrict__ coef,
                                                         const uint8_t* __restrict__ rmask,
                                                         const uint4* __restrict__ zq, FrameGeom G,
                                                         uint32_t* __restrict__ oslots,
