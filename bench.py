@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X DCT codec hot path (BASELINE.json `metric`).
 
-Workloads (--workload; `auto`, the default, picks chef-big at one rank and
-batch4k at more):
+Workloads (--workload; `auto`, the default, is chef-big at every rank count,
+so the driver's 1/2/4/8-GPU runs form one weak-scaling curve of one workload):
   chef-big  BASELINE.json configs[1], the metric's own configuration: a step
             is one DCT compress + decompress round trip of --inflight x
             --batch (default 3 x 24 = 72) 4032x3008 IYUV frames per rank
@@ -11,7 +11,9 @@ batch4k at more):
             chef-with-trumpet-big-DCT-50.myyuv), read from --input-frames
             (default: one per frame of a step, at least 24, rounded down to a
             multiple of --batch) distinct HBM copies: more bytes than the 256
-            MiB Infinity Cache, so the pixel reads come from HBM.  Weak scaling: every rank runs that batch.
+            MiB Infinity Cache, so the pixel reads come from HBM.  Weak scaling: every rank runs that batch,
+            and at N > 1 every rank's compressed streams are gathered to rank 0
+            inside the timed region (rank 0 checks the first, middle and last).
   batch4k   BASELINE.json configs[3]/[4]: a step is the batch of --frames
             (default 512) synthetic 3840x2160 IYUV frames, q=50 (frame f: the
             tiled chef-big frame with origin (8f mod 4032, 8f mod 3008),
@@ -19,12 +21,22 @@ batch4k at more):
             f mod N), compressed and decompressed where they live; at N > 1
             every rank's compressed streams are gathered to rank 0 inside the
             timed region.  The batch is fixed, so at N ranks each rank runs
-            --frames / N frames: strong scaling.  Every stream of the first
-            pass, and at N > 1 every gathered stream, is checked against
+            --frames / N frames: strong scaling.  Checked against
             tests/golden/batch4k_512.json (the oracle's payload and decode
-            sha256 per frame); every round trip's decode as well.
+            sha256 per frame): every stream and every decode of the untimed
+            first pass, and at N > 1 every gathered stream of the first and
+            the last timed step (the timed region's decodes are not compared).
+            At the default chef-big workload the same batch runs after the
+            timed region on all ranks as `side.batch4k` (at every N, so that
+            line is a strong-scaling curve of its own).
 value = megapixels (luma W*H) of all ranks' frames / max-over-ranks wall time
-of the K timed steps; frames and streams stay in HBM.
+of the K timed steps; frames and streams stay in HBM.  At N > 1 the line also
+carries `ranks`: per rank its wall time, its compute time (HIP events from the
+start of the timed region to the end of its last launch group), the exposed
+gather tail (wall - compute) and the stream bytes it sent (rank 0: received).
+Every rank's status (its codec's device errors, a payload past its slot) is
+all-gathered after the untimed pass and after the timed region; one failing
+rank makes every rank exit non-zero.
 
 Execution: launch groups of --batch frames go through the batch entry points
 (one launch per kernel covers the group), and --inflight groups are in flight
@@ -120,7 +132,7 @@ def parse(argv=None):
                     help="timed steps; chef-big: --inflight x --batch frames per rank, batch4k: the --frames batch")
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--workload", choices=("auto", "chef-big", "batch4k"), default="auto",
-                    help="auto: chef-big (configs[1]) at one rank, batch4k (configs[3]) at more")
+                    help="auto: chef-big (configs[1]) at every rank count (side.batch4k runs configs[3])")
     ap.add_argument("--frames", type=int, default=512,
                     help="batch4k: frames per step over all ranks (a multiple of the rank count)")
     ap.add_argument("--quality", type=int, default=50)
@@ -154,6 +166,9 @@ def parse(argv=None):
                          "72 copies, 1.31 GB at the default 3 x 24, larger than the 256 MiB Infinity Cache)")
     ap.add_argument("--cpu-codec", action="store_true",
                     help="tests only: the CPU restatement as the codec, host tensors, gloo (no GPU)")
+    ap.add_argument("--cpu-codec-fail", default="",
+                    help="tests only, with --cpu-codec: RANK:WHERE (warmup|timed) makes that rank's codec "
+                         "report an error there (timed: its first stream also gets a size past its slot)")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="only check the multi-rank launch: each rank joins a gloo group and "
                          "rank 0 prints the world size and an all_reduce (no GPU)")
@@ -402,6 +417,13 @@ class GpuCodec:
             if rc:
                 raise SystemExit(f"codec error {rc} ({myyuv_hip.strerror(rc)}) at block {bad}")
 
+    def marker(self):
+        """An event on the current stream (after join(): the end of every
+        launch group enqueued so far)."""
+        ev = self.torch.cuda.Event(enable_timing=True)
+        ev.record(self.torch.cuda.current_stream(self.dev))
+        return ev
+
     def join(self):
         for st in self.streams:
             self.torch.cuda.current_stream(self.dev).wait_stream(st)
@@ -418,11 +440,14 @@ class CpuCodec:
     """Tests only: the C restatement (oracle/) behind GpuCodec's interface, on
     host tensors, synchronous (no events)."""
 
-    def __init__(self, nf):
+    def __init__(self, nf, fail="", rank=0):
         import torch
         from oracle import oracle as O
         self.torch, self.O = torch, O
         self.streams = [None] * nf
+        r, _, where = fail.partition(":")
+        self.fail = where if fail and int(r) == rank else ""
+        self.phase = "warmup"
 
     def empty(self, shape, dtype=None):
         return self.torch.empty(shape, dtype=dtype or self.torch.uint8)
@@ -441,6 +466,8 @@ class CpuCodec:
                 raise SystemExit("codec error 5 (Output buffer too small for the compressed stream)")
             pay[b, :len(p)] = self.torch.frombuffer(bytearray(p), dtype=self.torch.uint8)
             size[b] = len(p)
+        if self.fail == "timed" and self.phase == "timed":
+            size[0] = cap + 4096  # a size past its slot: the gather must not hang on it
 
     def decompress(self, k, pay, size, cap, nb, w, h, q, out):
         fb = w * h * 3 // 2
@@ -453,7 +480,12 @@ class CpuCodec:
         return None
 
     def check(self):
-        pass
+        if self.fail and self.fail == self.phase:
+            raise SystemExit("codec error 5 (Output buffer too small for the compressed stream) "
+                             "[--cpu-codec-fail]")
+
+    def marker(self):
+        return None
 
     def join(self):
         pass
@@ -630,14 +662,19 @@ class Run:
     def timed(self, steps, dist, dev, gather_chunk):
         """K steps; at N > 1 the streams go to rank 0 (batch.ChunkedGather,
         chunks of about gather_chunk frames, each posted when its launch groups'
-        events fire).  Returns (seconds, gathered streams on rank 0 or None)."""
+        events fire).  Returns (seconds, gathered streams on rank 0 or None);
+        self.timing holds this rank's wall / compute / gather-tail seconds and
+        gathered bytes, self.gather_bad the ranks whose sizes passed a slot."""
         c = self.codec
         gat = None
         if self.world > 1:
             import batch
-            gat = batch.ChunkedGather(dist, self.world, self.rank, dev)
+            gat = batch.ChunkedGather(dist, self.world, self.rank, dev, cap=self.cap)
             dist.barrier()
         c.sync()
+        if isinstance(c, CpuCodec):
+            c.phase = "timed"
+        ev0 = c.marker()
         t0 = time.perf_counter()
         ngr = steps * self.ngroups
         evs, c0, nfr = [], 0, 0
@@ -653,11 +690,18 @@ class Run:
                     gat.add(list(range(c0, i1)), [self.d_pay[i] for i in range(c0, i1)], self.d_size[c0:i1], evs)
                     evs, c0, nfr = [], i1, 0
         c.join()
+        ev1 = c.marker()
+        t_host = time.perf_counter() - t0
         got = gat.finish(steps * self.n_local) if gat is not None else None
         c.sync()
+        wall = time.perf_counter() - t0
+        compute = ev0.elapsed_time(ev1) / 1e3 if ev0 is not None else t_host
+        self.timing = {"wall_s": wall, "compute_s": compute, "gather_tail_s": max(0.0, wall - compute),
+                       "gather_bytes": gat.bytes if gat is not None else 0}
+        self.gather_bad = sorted(gat.bad_ranks) if gat is not None else []
         if self.world > 1:
             dist.barrier()
-        return time.perf_counter() - t0, got
+        return wall, got
 
     def verify_gathered(self, got, steps):
         """Rank 0, N > 1: the gathered streams in global frame order."""
@@ -777,7 +821,7 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    name = args.workload if args.workload != "auto" else ("chef-big" if world == 1 else "batch4k")
+    name = args.workload if args.workload != "auto" else "chef-big"
     dist = None
     # launch shape 3 x 24: the launch groups' overflow lists (~200k blocks) take the CAP-16 tier;
     # chef-big driver shape 264.2k against 233.1k MP/s for 4 x 8 (two rounds, profiles/r3zzf_*, r3zzg_*,
@@ -791,7 +835,7 @@ def main(argv=None):
             import torch.distributed as dist
             dist.init_process_group("gloo")
         from oracle import oracle as O
-        codec = CpuCodec(nf)
+        codec = CpuCodec(nf, args.cpu_codec_fail, rank)
         raw = O.decompress(big.data, big.width, big.height, tuple(big.params))
     else:
         import myyuv_hip
@@ -808,7 +852,7 @@ def main(argv=None):
 
     run = Run(name, codec, raw, big, args, world, rank)
     run.alloc_slots(args.steps, args.warmup)
-    run.warmup(args.warmup)
+    checked(run.warmup, "the untimed pass", dist, world, rank, dev, args.warmup)
 
     # ---- timed region: K1 (the roofline kernel) event-stamped on every launch
     # group (the average is over the launches a rocprofv3 kernel trace of this
@@ -820,7 +864,7 @@ def main(argv=None):
         for c in stamped:
             c.profile(True, kernels=["fdct_quant"])
     t, got = run.timed(args.steps, dist, dev, args.gather_chunk)
-    codec.check()
+    checked(codec.check, "the timed region", dist, world, rank, dev, bad_ranks=run.gather_bad)
     stats = {}
     for c in stamped:
         for kname, (kms, kn) in c.kernel_stats().items():
@@ -831,10 +875,10 @@ def main(argv=None):
     if stamped and args.events_ctx0:
         stamped_frames = sum(run.group_desc(j)[2] for j in range(args.steps * run.ngroups)
                              if run.group_desc(j)[0] == 0)
+    ranks = None
     if world > 1:
-        tt = torch.tensor([t], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
+        ranks = rank_timings(dist, world, dev, run.timing)
+        t = max(r["wall_s"] for r in ranks)
         if rank == 0:
             run.verified["gathered"] = run.verify_gathered(got, args.steps)
     # per-kernel breakdown (all kernels stamped, one launch group at a time on
@@ -851,6 +895,11 @@ def main(argv=None):
     side = None
     if gpu and rank == 0 and not args.no_side:
         side = side_measurements(args, run, codec, raw, big, world, dev)
+    if gpu and not args.no_side and name == "chef-big" and run.q == 50:
+        # configs[3]/[4] on every rank (all ranks take part in its gather)
+        b4 = batch4k_side(args, codec, raw, big, world, rank, dist, dev)
+        if side is not None:
+            side["batch4k"] = b4
 
     if rank == 0:
         frames_all = world * args.steps * run.per_step
@@ -903,6 +952,10 @@ def main(argv=None):
                        "frames_per_launch": run.B, "payload_slot_bytes": run.cap,
                        **({"input_copies": run.nin, "payload_bytes": run.payload0} if name == "chef-big" else {})},
             "verified": run.verified,
+            **({"ranks": ranks, "gather": {
+                "bytes_to_rank0": sum(r["gather_bytes"] for r in ranks[1:]),
+                "ingress_gbs": round(sum(r["gather_bytes"] for r in ranks[1:]) / t / 1e9, 2),
+                "max_gather_tail_s": round(max(r["gather_tail_s"] for r in ranks), 6)}} if ranks else {}),
             "roofline": roof, "roofline_isolated": roof_iso, "roofline_decode_isolated": roof_dec,
             "cpu_baseline": cpu,
             "kernel_us": kernel_us or None,
@@ -962,28 +1015,77 @@ def side_measurements(args, run, codec, raw, big, world, dev):
     del bgra, d_iy
     if args.host_api_iters > 0:
         side["host_api"] = host_api_rate(myyuv_hip, raw, w, h, run.q, args.host_api_iters)
-    if run.name == "chef-big" and world == 1 and run.q == 50:
-        side["batch4k"] = batch4k_n1(args, codec, raw, big)
     return side
 
 
-def batch4k_n1(args, codec, raw, big):
-    """configs[3] on this one GPU: the 512-frame batch (every stream and decode
-    checked against the manifest in the first pass), then timed passes; the
-    N = 1 point of the batch4k workload's scaling curve."""
+def batch4k_side(args, codec, raw, big, world, rank, dist, dev):
+    """configs[3]/[4] after the timed region, on every rank: the 512-frame
+    batch dealt round-robin over the ranks (every stream and decode of the
+    first pass checked against the manifest on the rank that made it), then
+    timed passes with the streams gathered to rank 0 at N > 1 (rank 0 checks
+    the gathered streams of the first and last pass).  Strong scaling: the
+    same batch at every N, so these values form that workload's curve."""
     import torch
-    a = parse(["--workload", "batch4k", "--frames", str(args.frames), "--inflight", str(args.inflight)])
-    run = Run("batch4k", codec, raw, big, a, 1, 0)
+    a = parse(["--workload", "batch4k", "--frames", str(args.frames), "--inflight", str(args.inflight),
+               "--gather-chunk", str(args.gather_chunk)])
+    run = Run("batch4k", codec, raw, big, a, world, rank)
     passes = 3
     run.alloc_slots(passes, 1)
-    run.warmup(1)
-    t, _ = run.timed(passes, None, None, a.gather_chunk)
-    codec.check()
-    out = {"value": round(passes * run.n_total * run.mp / t, 2), "unit": "MP/s", "frames": run.n_total,
-           "passes": passes, "ms_per_pass": round(t / passes * 1e3, 3), "frames_per_launch": run.B,
-           "verified": run.verified["first_pass"]}
-    del run
+    checked(run.warmup, "side.batch4k's untimed pass", dist, world, rank, dev, 1)
+    t, got = run.timed(passes, dist, dev, a.gather_chunk)
+    checked(codec.check, "side.batch4k's timed passes", dist, world, rank, dev, bad_ranks=run.gather_bad)
+    out = None
+    if world > 1:
+        ranks = rank_timings(dist, world, dev, run.timing)
+        t = max(r["wall_s"] for r in ranks)
+    if rank == 0:
+        out = {"value": round(passes * run.n_total * run.mp / t, 2), "unit": "MP/s", "n_gpus": world,
+               "scaling": "strong", "frames": run.n_total, "passes": passes,
+               "ms_per_pass": round(t / passes * 1e3, 3), "frames_per_launch": run.B,
+               "verified": run.verified["first_pass"]}
+        if world > 1:
+            out["verified_gathered"] = run.verify_gathered(got, passes)
+            out["max_gather_tail_s"] = round(max(r["gather_tail_s"] for r in ranks), 6)
+    del run, got
     torch.cuda.empty_cache()
+    return out
+
+
+def checked(fn, what, dist, world, rank, dev, *a, bad_ranks=()):
+    """Runs fn(*a) (a codec check or the untimed pass); at N > 1 every rank's
+    outcome is all-gathered, and if any rank failed (or reported a payload
+    size past its slot, `bad_ranks`), every rank exits non-zero naming them."""
+    err = None
+    try:
+        fn(*a)
+    except (SystemExit, Exception) as e:  # noqa: BLE001 — reported to every rank below
+        err = str(e) or type(e).__name__
+    if world <= 1:
+        if err:
+            raise SystemExit(err)
+        return
+    import batch
+    codes = batch.agree_status(dist, 1 if err else 0, dev)
+    failed = sorted({r for r, c in enumerate(codes) if c} | set(bad_ranks))
+    if failed:
+        if err:
+            log(f"rank {rank}: {err}")
+        raise SystemExit(f"bench.py: rank(s) {failed} failed in {what}"
+                         + (f" (rank {rank}: {err})" if err else ""))
+
+
+def rank_timings(dist, world, dev, timing):
+    """Every rank's timing record (Run.timing) on every rank, in rank order."""
+    import torch
+    keys = ("wall_s", "compute_s", "gather_tail_s", "gather_bytes")
+    t = torch.tensor([float(timing[k]) for k in keys], dtype=torch.float64, device=dev)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    out = []
+    for r, p in enumerate(parts):
+        v = p.cpu().tolist()
+        out.append({"rank": r, "wall_s": round(v[0], 6), "compute_s": round(v[1], 6),
+                    "gather_tail_s": round(v[2], 6), "gather_bytes": int(v[3])})
     return out
 
 

@@ -116,12 +116,16 @@ int myyuv_gpu_dct_decompress_device(myyuv_hip_handle h, const void* d_payload,
  * of frame f > 0 reports f * blocks_per_frame.  Each frame's bytes are those
  * of the single-frame call.
  * Workspace (myyuv_hip_reserve_batch reserves it up front; the calls grow it
- * on demand): about 460 B per 8x8 block of the batch — the encoder's stage
- * (160 B: a tile's chunks, kMaxChunk per block) and overflow slots (160 B per
- * block: any block may exceed 8 distinct symbols, as nearly all of a noise
- * frame's do, so the slots cannot be sized from a typical list), plus the
- * coefficients (128 B) and small per-block arrays.  A 7-frame 4032x3008 batch
- * takes ~0.9 GB, a 16-frame 8192x8192 batch ~12 GB (of 288 GB). */
+ * on demand): about 466 B per 8x8 block of the batch — the encoder's stage
+ * (160 B: a tile's chunks, kMaxChunk per block, rounded up to whole 4-tile
+ * K2 windows) and overflow slots (160 B per block: any block may exceed 8
+ * distinct symbols, as nearly all of a noise frame's do, so the slots cannot
+ * be sized from a typical list), the coefficients (128 B), the chunk offsets
+ * (u32 srcoff, 4 B), the decoder's group offsets (4 B), the overflow worklist
+ * (8 B: the CAP-16 tier's list and its rest list), the sizes and row masks
+ * (2 B).  A 4032x3008 frame (284,256 blocks) takes ~132 MB: the bench's
+ * 24-frame launch groups ~3.2 GB per context, 3 contexts ~9.5 GB; a 16-frame
+ * 8192x8192 batch ~11.7 GB (of 288 GB). */
 int myyuv_hip_reserve_batch(myyuv_hip_handle h, uint32_t width, uint32_t height, uint32_t nframes);
 int myyuv_gpu_dct_compress_batch_device(myyuv_hip_handle h, const void* d_iyuv, uint32_t nframes,
                                         uint32_t width, uint32_t height, const uint8_t quality[3],

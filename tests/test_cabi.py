@@ -81,3 +81,33 @@ def test_host_library_and_cli_are_built():
                 "myyuv::YUV::compress_map", "myyuv::YUV::decompress_map", "myyuv::YUV::load",
                 "myyuv::YUV::dump"):
         assert sym in out, sym
+
+
+def test_into_calls_check_their_buffers():
+    """compress_into / decompress_into hand the caller's arrays to the C ABI
+    as raw pointers: short, strided, non-uint8 or read-only buffers are refused
+    before any call (no GPU needed: the checks precede it)."""
+    import numpy as np
+    import myyuv_hip
+    c = myyuv_hip.Codec.__new__(myyuv_hip.Codec)
+    c._h = None
+    w, h = 16, 16
+    fb = w * h * 3 // 2
+    good = np.zeros(fb, np.uint8)
+    out = np.zeros(4096, np.uint8)
+    bad_inputs = [np.zeros(fb - 1, np.uint8),                 # short frame
+                  np.zeros(2 * fb, np.uint8)[::2],           # strided
+                  np.zeros(fb, np.int16),                    # not uint8
+                  bytes(fb)]                                 # not an ndarray
+    for a in bad_inputs:
+        with pytest.raises(ValueError):
+            c.compress_into(a, w, h, (50, 50, 50), out)
+    ro = np.zeros(4096, np.uint8)
+    ro.flags.writeable = False
+    for o in (np.zeros(8192, np.uint8)[::2], np.zeros(4096, np.uint16), ro):
+        with pytest.raises(ValueError):
+            c.compress_into(good, w, h, (50, 50, 50), o)
+    with pytest.raises(ValueError):
+        c.decompress_into(np.zeros(64, np.uint8), w, h, (50, 50, 50), np.zeros(fb - 1, np.uint8))
+    with pytest.raises(ValueError):
+        c.decompress_into(np.zeros(128, np.uint8)[::2], w, h, (50, 50, 50), np.zeros(fb, np.uint8))

@@ -203,3 +203,47 @@ def test_bench_n2_loop_cpu_codec(workload, extra):
     assert "first_pass" in d["verified"]
     if workload == "batch4k":
         assert "tests/golden/batch4k_512.json" in d["verified"]["gathered"]
+    # per-rank compute and gather time, separately (the N > 1 line's `ranks`)
+    ranks = d["ranks"]
+    assert [r["rank"] for r in ranks] == [0, 1]
+    for r in ranks:
+        assert r["wall_s"] > 0 and 0 < r["compute_s"] <= r["wall_s"] + 1e-6
+        assert abs(r["gather_tail_s"] - max(0.0, r["wall_s"] - r["compute_s"])) < 1e-5
+    assert ranks[1]["gather_bytes"] > 0 and ranks[0]["gather_bytes"] == ranks[1]["gather_bytes"]
+    assert d["gather"]["bytes_to_rank0"] == ranks[1]["gather_bytes"]
+    assert abs(d["ms_per_step"] * steps / 1e3 - max(r["wall_s"] for r in ranks)) < 1e-3
+
+
+def test_bench_auto_workload_is_one_curve():
+    """The default workload is chef-big at every rank count: the driver's
+    1/2/4/8-GPU runs measure one weak-scaling curve of one workload."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-codec",
+                        "--warmup", "1", "--batch", "1", "--inflight", "1", "--gather-chunk", "1", "--steps", "1",
+                        "--input-frames", "1"],
+                       capture_output=True, text=True, timeout=600, env=_bench_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _bench_json(r.stdout)
+    assert d["scaling"] == "weak" and "BASELINE configs[1]" in d["config"]["workload"]
+
+
+@pytest.mark.parametrize("where", ["warmup", "timed"])
+def test_bench_rank_failure_fails_every_rank(where):
+    """One rank's codec failure (forced with --cpu-codec-fail) ends every rank
+    with a non-zero status naming it, instead of leaving rank 0 blocked in a
+    collective.  In the timed case that rank also reports a stream size past
+    its payload slot; the gather clamps it identically on both ranks, so the
+    point-to-point phase still completes and the status exchange decides."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-codec",
+                        "--cpu-codec-fail", f"1:{where}", "--warmup", "1", "--batch", "1", "--inflight", "1",
+                        "--gather-chunk", "1", "--steps", "1", "--input-frames", "1"],
+                       capture_output=True, text=True, timeout=300, env=_bench_env(), cwd=ROOT)
+    assert r.returncode != 0
+    phase = "the untimed pass" if where == "warmup" else "the timed region"
+    # both ranks report the verdict (rank 0 about rank 1, rank 1 with its error)
+    assert f"rank(s) [1] failed in {phase}" in r.stderr, r.stderr[-3000:]
+    assert "(rank 1: codec error 5" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

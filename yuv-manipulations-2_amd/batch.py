@@ -16,6 +16,18 @@ The codec itself is a callable, so the same driver runs the HIP codec
 import torch
 
 
+def agree_status(dist, code, device):
+    """Every rank's status code (0 = ok) on every rank, in rank order: an
+    all_gather of one int64 per rank.  The bench calls it after its untimed
+    pass and after the timed region, so a rank whose codec failed makes every
+    rank exit with the same verdict instead of leaving the others blocked in
+    the next collective (SURVEY.md §5 "Batch: a per-rank status allgather")."""
+    t = torch.tensor([int(code)], dtype=torch.int64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [int(p.item()) for p in parts]
+
+
 def shard(n_frames, world, rank):
     """Frame f goes to rank f mod world (round-robin)."""
     return list(range(rank, n_frames, world))
@@ -91,10 +103,20 @@ class ChunkedGather:
 
     Local frame i of rank r is global frame r + world * i (shard()).  With
     CPU tensors (gloo tests) there are no streams and every step is eager.
+
+    Sizes are clamped to [0, cap] (the payload slot) on every rank before any
+    transfer is sized, so a failed frame (a size past its slot or negative)
+    cannot make a sender and rank 0 disagree on a message length, which would
+    hang the point-to-point phase; every rank sees the same all-gathered
+    sizes, so `bad_ranks` (the ranks that reported such a size) is the same
+    set everywhere and the caller's status exchange fails them all cleanly.
     """
 
-    def __init__(self, dist, world, rank, device):
+    def __init__(self, dist, world, rank, device, cap=None):
         self.dist, self.world, self.rank, self.device = dist, world, rank, device
+        self.cap = cap
+        self.bad_ranks = set()
+        self.bytes = 0  # bytes this rank sent (rank 0: received) so far
         self.cuda = device.type == "cuda"
         self.side = torch.cuda.Stream(device) if self.cuda else None
         self.pending = []  # (local indices, payloads, host sizes [world][k], ready event)
@@ -135,6 +157,11 @@ class ChunkedGather:
         if ev is not None:
             ev.synchronize()
         hs = hs.tolist()
+        for r, row in enumerate(hs):
+            for j, n in enumerate(row):
+                if n < 0 or (self.cap is not None and n > self.cap):
+                    self.bad_ranks.add(r)
+                    row[j] = min(max(n, 0), self.cap if self.cap is not None else 0)
         dist, rank = self.dist, self.rank
         with self._stream():
             if rank != 0:
@@ -142,6 +169,7 @@ class ChunkedGather:
                 if total > 0:
                     packed = torch.cat([p[:n] for p, n in zip(payloads, hs[rank])])
                     self.keep.append(packed)  # alive until finish() has waited
+                    self.bytes += total
                     self.works += dist.batch_isend_irecv([dist.P2POp(dist.isend, packed, 0)])
                 return
             own = {i: p[:n] for i, p, n in zip(local, payloads, hs[0])}
@@ -149,6 +177,7 @@ class ChunkedGather:
             for r in range(1, self.world):
                 total = sum(hs[r])
                 if total > 0:
+                    self.bytes += total
                     bufs[r] = torch.empty(total, dtype=torch.uint8, device=self.device)
                     ops.append(dist.P2POp(dist.irecv, bufs[r], r))
             if ops:

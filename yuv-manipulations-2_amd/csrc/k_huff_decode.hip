@@ -589,13 +589,16 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
 #pragma unroll 1
   for (uint32_t u = 0; 16u * u < nrest; u++) {
     // the unit's blocks: compacted positions 16u .. 16u+15 (slots past the
-    // last block are zero, so they do not keep steps alive)
+    // last block are zero, so they do not keep steps alive).  Slot `lane`
+    // (< 16) is zeroed by lane `lane` whether or not that lane also writes a
+    // compacted block: the two slots differ (rrank < nrest <= 16u + lane).
     const bool mine = D.live && !isdc && (rrank >> 4) == u;
     if (mine) {
       uint4* img = reinterpret_cast<uint4*>(tile + (rrank & 15u) * xf::kTile);
 #pragma unroll
       for (int c = 0; c < 8; c++) img[c] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
-    } else if (lane < 16u && 16u * u + lane >= nrest) {
+    }
+    if (lane < 16u && 16u * u + lane >= nrest) {
       uint4* img = reinterpret_cast<uint4*>(tile + lane * xf::kTile);
 #pragma unroll
       for (int c = 0; c < 8; c++) img[c] = make_uint4(0u, 0u, 0u, 0u);

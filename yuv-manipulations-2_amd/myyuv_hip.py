@@ -117,6 +117,17 @@ def _u8(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
 
 
+def _u8_array(a, name, writable=False):
+    """The caller's buffer as-is (no copy): a C-contiguous uint8 ndarray, else
+    ValueError (a strided or wider-typed array would hand the C ABI the wrong
+    bytes, and a copy of `out` would drop the result)."""
+    if not isinstance(a, np.ndarray) or a.dtype != np.uint8 or not a.flags.c_contiguous:
+        raise ValueError(f"{name}: a C-contiguous numpy uint8 array is required")
+    if writable and not a.flags.writeable:
+        raise ValueError(f"{name}: read-only array")
+    return a
+
+
 def _q(q):
     return np.ascontiguousarray(np.array(q, dtype=np.int64).astype(np.uint8))
 
@@ -173,9 +184,15 @@ class Codec:
 
     def compress_into(self, iyuv, w, h, q, out):
         """IYUV numpy buffer -> payload written into the caller's numpy buffer
-        `out` (no per-call allocation); returns the payload size."""
+        `out` (no per-call allocation); returns the payload size.  Both must be
+        C-contiguous uint8 arrays: `iyuv` at least W*H*3/2 bytes, `out` sized
+        by its byte count (a short `out` fails with E_CAPACITY)."""
+        src = _u8_array(iyuv, "iyuv")
+        dst = _u8_array(out, "out", writable=True)
+        if src.nbytes < w * h * 3 // 2:
+            raise ValueError("frame smaller than W*H*3/2")
         size = ctypes.c_uint32(0)
-        rc = load().myyuv_gpu_dct_compress(self._h, _u8(iyuv), w, h, _u8(_q(q)), _u8(out), out.size,
+        rc = load().myyuv_gpu_dct_compress(self._h, _u8(src), w, h, _u8(_q(q)), _u8(dst), dst.nbytes,
                                            ctypes.byref(size))
         if rc:
             raise CodecError(rc)
@@ -183,11 +200,13 @@ class Codec:
 
     def decompress_into(self, payload, w, h, q, out):
         """payload numpy buffer -> IYUV frame written into the caller's numpy
-        buffer `out` (W*H*3/2 bytes)."""
-        if out.size < w * h * 3 // 2:
+        buffer `out` (at least W*H*3/2 bytes); both C-contiguous uint8."""
+        src = _u8_array(payload, "payload")
+        dst = _u8_array(out, "out", writable=True)
+        if dst.nbytes < w * h * 3 // 2:
             raise ValueError("output smaller than W*H*3/2")
         bad = ctypes.c_int64(-1)
-        rc = load().myyuv_gpu_dct_decompress(self._h, _u8(payload), payload.size, w, h, _u8(_q(q)), _u8(out),
+        rc = load().myyuv_gpu_dct_decompress(self._h, _u8(src), src.nbytes, w, h, _u8(_q(q)), _u8(dst),
                                              ctypes.byref(bad))
         if rc:
             raise CodecError(rc, bad.value)
