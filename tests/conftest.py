@@ -38,18 +38,21 @@ def codec(request):
     """A codec context per kernel arrangement: "split" (K1 -> K2 and K5 -> K6
     through HBM) and "fused" (the single-pass encoder k_encode_tile and the
     single-pass decoder k_decode_idct, the decoder's default; MYYUV_ENCODER /
-    MYYUV_DECODER are read when the context is created).  Every test taking
-    `codec` runs on both."""
+    MYYUV_DECODER are read when the context is created).  The stream writer
+    follows: "split" takes the default k_stream_out_coop, "fused" the
+    lane-per-block k_stream_out (MYYUV_STREAM_OUT).  Every test taking `codec`
+    runs on both."""
     import myyuv_hip
 
-    keys = ("MYYUV_ENCODER", "MYYUV_DECODER")
-    old = {k: os.environ.get(k) for k in keys}
-    for k in keys:
-        os.environ[k] = request.param
+    vals = {"MYYUV_ENCODER": request.param, "MYYUV_DECODER": request.param,
+            "MYYUV_STREAM_OUT": "coop" if request.param == "split" else "lane"}
+    old = {k: os.environ.get(k) for k in vals}
+    for k, v in vals.items():
+        os.environ[k] = v
     try:
         c = myyuv_hip.Codec(0)
     finally:
-        for k in keys:
+        for k in vals:
             if old[k] is None:
                 del os.environ[k]
             else:

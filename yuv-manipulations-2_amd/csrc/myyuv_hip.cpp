@@ -51,6 +51,8 @@ __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*,
                              uint32_t, unsigned long long*);
 __global__ void k_stream_out(const uint32_t*, const uint32_t*, const uint8_t*, const uint32_t*,
                              const uint32_t*, FrameGeom, uint8_t*, uint32_t);
+__global__ void k_stream_out_coop(const uint32_t*, const uint32_t*, const uint8_t*, const uint32_t*,
+                                  const uint32_t*, FrameGeom, uint8_t*, uint32_t);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
                               uint4*, uint8_t*, unsigned long long*);
@@ -194,6 +196,9 @@ struct myyuv_hip_ctx {
   // decoder: the fused k_decode_idct (default), or K5 -> K6 through HBM
   // (MYYUV_DECODER=split)
   bool fused_dec = true;
+  // stream writer: k_stream_out_coop (copy split by output dwords) or the
+  // lane-per-block k_stream_out (MYYUV_STREAM_OUT=coop|lane)
+  bool coop_out = true;
   // chained scan (k_chain.hpp): per-tile status words tagged with the launch
   // epoch, counted here
   DevBuf status;
@@ -319,8 +324,9 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   const uint32_t ntiles = ceil_div(G.cum[3], kScanTile);
   int e = 0;
   e |= c->coef.grow((size_t)nwaves * kCoefQuadsPerWave * 16);  // natural-order quads
-  e |= c->stage.grow((size_t)win_tiles_alloc(nf * G.tcum[3]) * kTileCap);
-  e |= c->oslots.grow((size_t)nblk * kMaxChunk);
+  // (+64 B: the stream writers read a word past a chunk's last one)
+  e |= c->stage.grow((size_t)win_tiles_alloc(nf * G.tcum[3]) * kTileCap + 64);
+  e |= c->oslots.grow((size_t)nblk * kMaxChunk + 64);
   e |= c->tinfo.grow((size_t)nf * G.tcum[3] * kTInfoWords * 4);
   e |= c->srcoff.grow((size_t)nblk * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
@@ -440,7 +446,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   }
   e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(256), s, c->tinfo.as<uint32_t>(), G,
               static_cast<uint8_t*>(d_out), cap, d_size, err);
-  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
+  e |= launch(c, MYYUV_K_COMPACT, c->coop_out ? k_stream_out_coop : k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
               c->stage.as<const uint32_t>(), c->tinfo.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
               c->srcoff.as<const uint32_t>(), c->oslots.as<const uint32_t>(), G, static_cast<uint8_t*>(d_out),
               cap);
@@ -612,6 +618,8 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
         c->fused = v && std::strcmp(v, "fused") == 0;
         const char* d = std::getenv("MYYUV_DECODER");
         c->fused_dec = !(d && std::strcmp(d, "split") == 0);
+        const char* so = std::getenv("MYYUV_STREAM_OUT");
+        c->coop_out = !(so && std::strcmp(so, "lane") == 0);
       }
       // tuning knobs (diagnostic; default 100): K1 / K6 grids as a percentage
       // of the resident workgroups, leaving wave slots to other launch groups
