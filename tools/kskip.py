@@ -1,7 +1,8 @@
 """Diagnostic: each kernel's share of the pipelined bench configuration
-(3 streams x 7-frame launches, chef-big q50): throughput with that kernel's
-launches skipped (myyuv_debug_skip_kernels; identical frames, so the buffers
-still hold what the last real launch wrote)."""
+(KSKIP_NF streams x KSKIP_B-frame launches, default the bench's 3 x 24,
+chef-big q50): throughput with that kernel's launches skipped
+(myyuv_debug_skip_kernels; identical frames, so the buffers still hold what
+the last real launch wrote)."""
 import ctypes
 import os
 import sys
@@ -13,7 +14,9 @@ import torch  # noqa: E402
 import myyuv_file  # noqa: E402
 import myyuv_hip  # noqa: E402
 
-NF, B, GROUPS = 3, 7, 60
+NF = int(os.environ.get("KSKIP_NF", "3"))
+B = int(os.environ.get("KSKIP_B", "24"))
+GROUPS = int(os.environ.get("KSKIP_GROUPS", "30"))
 g = myyuv_file.YUVFile.load(os.path.join(ROOT, "tests/golden/chef-with-trumpet-big-DCT-50.myyuv"))
 w, h = g.width, g.height
 L = myyuv_hip.load()

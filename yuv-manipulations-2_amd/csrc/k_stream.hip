@@ -336,9 +336,11 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
 
 // The same tile -> stream step with the copy split by output dwords instead of
 // by chunks (round 4): lane-per-block k_stream_out runs every lane's copy loop
-// to the longest chunk of its wave, a few long chunks among many 7-byte ones.
-// Here the chunks' offsets, source words and headers go to LDS, then the
-// workgroup walks the tile's output dwords, 256 at a time, lane i taking
+// to the longest chunk of its wave, a few long chunks among many 7-byte ones,
+// and its waves hold their slots for it (12.9 % of all wave-cycles for 6.2 %
+// of the VALU work, profiles/r3zb_sq_counters.txt).  Here the chunks'
+// offsets and sources go to LDS (one load round trip: size and srcoff), then
+// the workgroup walks the tile's output dwords, 256 at a time, lane i taking
 // dwords i, i + 256, ...:
 //   * the chunk holding a dword's first byte: every chunk marks the dword
 //     holding its own first byte (chunks are >= 7 bytes, so at most one starts
@@ -346,13 +348,16 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
 //     last chunk starting at or before it, and one offset compare settles a
 //     chunk starting mid-dword;
 //   * the dword: two source words of that chunk, funnel-shifted; bytes past
-//     the chunk's end are the next chunk's first (its header, <= 3 bytes).
+//     the chunk's end are the next chunk's first (its header, <= 3 bytes),
+//     whose source words are loaded in the same round trip.
 // Ownership rules as k_stream_out: the dword holding the tile's first byte
 // belongs to the previous tile (completed there with this tile's first
 // header), except at a plane's first chunk (byte stores: it meets the size
 // array); a plane's last dword is written with byte stores (it meets the next
 // plane's header).  Dwords are claimed in rounds of kCoopRound (one round for
-// a 4032x3008 q=50 tile, ~3 KB).
+// a 4032x3008 q=50 tile, ~3 KB).  The rules were checked on 3,000 random
+// tile sequences by a host model before the kernel was written: every byte
+// written exactly once, with its chunk's value.
 namespace {
 constexpr uint32_t kCoopRound = 1024;  // output dwords per round (4 per lane)
 }
@@ -364,8 +369,7 @@ __global__ __launch_bounds__(256) void k_stream_out_coop(const uint32_t* __restr
                                                          const uint32_t* __restrict__ oslots, FrameGeom G,
                                                          uint8_t* __restrict__ out, uint32_t cap) {
   __shared__ uint32_t s_off[kK2Group + 1];  // tile-local byte offset of chunk c (block order); [nloc] = total
-  __shared__ uint32_t s_so[kK2Group];       // srcoff of chunk c
-  __shared__ uint32_t s_hdr[kK2Group + 1];  // chunk c's first 3 bytes; [nloc]: the next tile's first chunk's
+  __shared__ uint32_t s_so[kK2Group + 1];   // srcoff of chunk c; [nloc]: the next tile's first block's
   __shared__ uint32_t s_mark[kCoopRound];   // per dword of the round: last chunk (+1) starting at or before it
   __shared__ uint32_t s_w[4], s_carry;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -376,27 +380,31 @@ __global__ __launch_bounds__(256) void k_stream_out_coop(const uint32_t* __restr
   const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
   const uint32_t gb = f * G.cum[3] + g0;
   out += (size_t)f * cap;
-  const uint32_t* wstage = stage + (size_t)win_first_tile(T) * (kTileCap / 4);
   const uint32_t x = tinfo[(size_t)T * kTInfoWords + kTInfoPrefix];  // the tile's content prefix
   const uint32_t ppre = tinfo[((size_t)f * ntile + G.tcum[p]) * kTInfoWords + kTInfoPrefix];
   const bool plane_end = g0 + nloc == G.cum[p + 1];
   const bool plane_first = g0 == G.cum[p];
-  // ---- phase 1, lane per block: size, source, header, offsets
+  // chunk c's source words and byte shift (c == nloc: the next tile's first chunk)
+  auto chunk_src = [&](uint32_t c, uint32_t so, uint32_t& sh) -> const uint32_t* {
+    if (so == kSrcOverflow) {
+      sh = 0;
+      return oslots + (size_t)(gb + c) * kSlotWords;
+    }
+    sh = so & 3u;
+    return stage + (size_t)win_first_tile(c < nloc ? T : T + 1) * (kTileCap / 4) + (so >> 2);
+  };
+  // the first 4 bytes at a chunk's start (its header): two source words
+  auto head_of = [&](uint32_t c) -> uint32_t {
+    uint32_t sh;
+    const uint32_t* s1 = chunk_src(c, s_so[c], sh);
+    const uint32_t a = s1[0], b = s1[1];
+    return sh ? (a >> (8 * sh)) | (b << (32 - 8 * sh)) : a;
+  };
+  // ---- phase 1, lane per block: size, source, offsets (one load round trip)
   const bool live = tid < nloc;
   const uint32_t sz = live ? sizes[gb + tid] : 0u;
   const uint32_t so = live ? srcoff[gb + tid] : 0u;
-  // the header of the lane's chunk, and (lane nloc - 1, the plane going on)
-  // the next tile's first chunk's
-  auto header_at = [&](uint32_t T1, uint32_t g, uint32_t so1) -> uint32_t {
-    const uint32_t* s1 = so1 == kSrcOverflow ? oslots + (size_t)g * kSlotWords
-                                             : stage + (size_t)win_first_tile(T1) * (kTileCap / 4) + (so1 >> 2);
-    const uint32_t r1 = so1 == kSrcOverflow ? 0u : so1 & 3u;
-    const uint32_t a = s1[0];
-    return r1 ? (a >> (8 * r1)) | (s1[1] << (32 - 8 * r1)) : a;
-  };
-  const uint32_t hdr = live ? header_at(T, gb + tid, so) : 0u;
-  uint32_t nxh = 0;
-  if (tid == nloc - 1 && !plane_end) nxh = header_at(T + 1, gb + nloc, srcoff[gb + nloc]);
+  const uint32_t so_next = (tid == nloc - 1 && !plane_end) ? srcoff[gb + nloc] : 0u;
   const uint32_t incl = wave_inclusive_scan(sz);
   if (lane == 63) s_w[wave] = incl;
   __syncthreads();
@@ -407,11 +415,10 @@ __global__ __launch_bounds__(256) void k_stream_out_coop(const uint32_t* __restr
   if (live) {
     s_off[tid] = o;
     s_so[tid] = so;
-    s_hdr[tid] = hdr;
   }
   if (tid == nloc - 1) {
     s_off[nloc] = tot;
-    s_hdr[nloc] = nxh;
+    s_so[nloc] = so_next;
   }
   // ---- chunk_size[] bytes (DCTYUVPlane layout: after the plane's 8-byte header)
   const uint64_t spos = 12ull + 8ull * (p + 1) + ppre + g0;
@@ -421,13 +428,15 @@ __global__ __launch_bounds__(256) void k_stream_out_coop(const uint32_t* __restr
   const uint64_t D0 = (P0 + 3) >> 2;                              // the first dword the tile owns
   const uint32_t J = (uint32_t)(((P0 + tot - 1) >> 2) - D0 + 1);  // dwords the tile owns
   const uint32_t lead = (uint32_t)(4 * D0 - P0);                  // chunk 0's bytes before dword D0
-  if (plane_first && lead && tid == 0) {  // the dword before is shared with the size array
-    for (uint32_t k = 0; k < lead; k++)
-      if (P0 + k < cap) out[P0 + k] = (uint8_t)(hdr >> (8 * k));
-  }
   // chunk tid's first dword, relative to D0 (chunk 0 marks dword 0)
   const uint32_t jc = live ? (tid == 0 ? 0u : (uint32_t)(((P0 + o) >> 2) - D0)) : ~0u;
   if (tid == 0) s_carry = 0;
+  __syncthreads();  // (s_off / s_so complete)
+  if (plane_first && lead && tid == 0) {  // the dword before is shared with the size array
+    const uint32_t h = head_of(0);
+    for (uint32_t k = 0; k < lead; k++)
+      if (P0 + k < cap) out[P0 + k] = (uint8_t)(h >> (8 * k));
+  }
   for (uint32_t R = 0; R < J; R += kCoopRound) {
     // ---- marks, then a workgroup max-scan (4 per lane)
 #pragma unroll
@@ -458,7 +467,9 @@ __global__ __launch_bounds__(256) void k_stream_out_coop(const uint32_t* __restr
     for (uint32_t k = 0; k < 4; k++) s_mark[4 * tid + k] = max(pm, m[k]);
     __syncthreads();
     if (tid == 0) s_carry = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
-    // ---- the round's dwords: lane tid takes R + tid + 256 k
+    // ---- the round's dwords: lane tid takes R + tid + 256 k; the source
+    // words of its chunk and, when the dword runs past the chunk, of the
+    // next chunk's header are loaded together (one round trip)
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
       const uint32_t j = R + tid + 256u * k;
@@ -472,23 +483,17 @@ __global__ __launch_bounds__(256) void k_stream_out_coop(const uint32_t* __restr
         oc = s_off[c];
       }
       const uint32_t avail = s_off[c + 1] - b;  // chunk c's bytes from the dword's start
-      const uint32_t sc = s_so[c];
-      const uint32_t* src;
-      uint32_t r;
-      if (sc == kSrcOverflow) {
-        src = oslots + (size_t)(gb + c) * kSlotWords;
-        r = b - oc;
-      } else {
-        src = wstage + (sc >> 2);
-        r = (sc & 3u) + (b - oc);
-      }
-      const uint32_t wi = r >> 2, q = r & 3u;
+      uint32_t sh;
+      const uint32_t* src = chunk_src(c, s_so[c], sh);
+      const uint32_t r = sh + (b - oc), wi = r >> 2, q = r & 3u;
       const uint32_t a0 = src[wi], a1 = src[wi + 1];  // (buffers padded: wi + 1 stays inside)
+      const bool more = avail < 4 && (c + 1 < nloc || !plane_end);
+      const uint32_t hn = more ? head_of(c + 1) : 0u;
       uint32_t v = q ? (a0 >> (8 * q)) | (a1 << (32 - 8 * q)) : a0;
       const uint64_t pos = 4 * D;
       if (avail < 4) {
-        if (c + 1 < nloc || !plane_end) {
-          v = (v & ((1u << (8 * avail)) - 1u)) | (s_hdr[c + 1] << (8 * avail));
+        if (more) {
+          v = (v & ((1u << (8 * avail)) - 1u)) | (hn << (8 * avail));
         } else {  // the plane's last bytes: the next plane's header follows
           for (uint32_t i = 0; i < avail; i++)
             if (pos + i < cap) out[pos + i] = (uint8_t)(v >> (8 * i));
