@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-kernel times of one 7-frame launch group (chef-big q50,
+"""Diagnostic: per-kernel times of one 7-frame (K1AB_B) launch group (chef-big q50,
 batch entry points, kernels alone on the GPU, HIP events, no correctness
 checks) for the library builds given as arguments (directories holding a
 libmyyuv_hip.so, "default", or VAR=value: the in-tree build with that
@@ -18,7 +18,7 @@ sys.path[:0] = [%r, %r]
 import torch, myyuv_file, myyuv_hip
 from oracle import oracle as O
 g = myyuv_file.YUVFile.load(os.path.join(%r, "tests", "golden", "chef-with-trumpet-big-DCT-50.myyuv"))
-w, h, B = g.width, g.height, 7
+w, h, B = g.width, g.height, int(os.environ.get("K1AB_B", "7"))
 raw = O.decompress(g.data, w, h, tuple(g.params))
 dev = torch.device("cuda", 0)
 c = myyuv_hip.Codec(0)

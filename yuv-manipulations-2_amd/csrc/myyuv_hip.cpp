@@ -342,7 +342,8 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->psize.grow(4);
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
   // [0], [1]: overflow counts, then K2's list and (single frames) the CAP-16 tier's (launch_overflow)
-  e |= c->work.grow((size_t)nblk * (nf == 1 || MYYUV_R16_BATCH ? 8 : 4) + 256);
+  // (then the CAP-16 tier's rest list, nblk words, and the u16 sort keys of K2's list: r16_keys)
+  e |= c->work.grow((size_t)nblk * 10 + 256);
   const size_t st_bytes = (size_t)nf * (ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
@@ -400,8 +401,12 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
     // work[1], the tier's count (its own node: a store in K1's prologue
     // shifted K1's loop and cost it 5 %, profiles/r3zx_*)
     e |= hipMemsetAsync(count2, 0, 4, s) != hipSuccess;
-    const uint32_t r16 = ceil_div(nblk, kWave) < kR16Grid ? ceil_div(nblk, kWave) : kR16Grid;
-    e |= launch(c, MYYUV_K_HUFF_R16, k_huff_encode_r16, dim3(r16), dim3(kWave), s, c->coef.as<const uint4>(),
+#if MYYUV_R16_SORT
+    const uint32_t r16 = std::min(ceil_div(nblk, kR16Win), kR16SortGrid), r16_block = kR16Win;
+#else
+    const uint32_t r16 = ceil_div(nblk, kWave) < kR16Grid ? ceil_div(nblk, kWave) : kR16Grid, r16_block = kWave;
+#endif
+    e |= launch(c, MYYUV_K_HUFF_R16, k_huff_encode_r16, dim3(r16), dim3(r16_block), s, c->coef.as<const uint4>(),
                 c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G, c->oslots.as<uint32_t>(),
                 c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
                 list2, count2);
