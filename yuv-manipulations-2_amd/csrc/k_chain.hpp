@@ -32,13 +32,27 @@ __device__ __forceinline__ int parse_stream(const uint8_t* __restrict__ in, uint
   if (size <= 12) return 6;
   uint32_t ps[3];
   for (int p = 0; p < 3; p++) ps[p] = rd32(4 * p);
+  // the three plane headers are loaded together (two load round trips in all,
+  // not one per plane): positions clamped into the stream, the values used
+  // only once the checks below have passed
+  uint32_t hw[6];
+  {
+    const uint64_t last = size - 8ull;
+    const uint64_t o[3] = {12ull, 12ull + ps[0], 12ull + ps[0] + ps[1]};
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+      const uint64_t a = o[p] < last ? o[p] : last;
+      hw[2 * p] = rd32(a);
+      hw[2 * p + 1] = rd32(a + 4);
+    }
+  }
   if (12ull + ps[0] + ps[1] + ps[2] > size) return 6;
   uint64_t poff = 12;
   uint32_t hn[3];
   for (int p = 0; p < 3; p++) {
     if (ps[p] <= 8) return 7;
-    hn[p] = rd32(poff);
-    const uint32_t hc = rd32(poff + 4);
+    hn[p] = hw[2 * p];
+    const uint32_t hc = hw[2 * p + 1];
     if (hn[p] == 0) return 8;
     if (hc == 0) return 9;
     if (8ull + hn[p] + hc > ps[p]) return 7;
