@@ -38,14 +38,11 @@ def codec(request):
     """A codec context per kernel arrangement: "split" (K1 -> K2 and K5 -> K6
     through HBM) and "fused" (the single-pass encoder k_encode_tile and the
     single-pass decoder k_decode_idct, the decoder's default; MYYUV_ENCODER /
-    MYYUV_DECODER are read when the context is created).  The stream writer
-    follows: "split" takes the default k_stream_out_coop, "fused" the
-    lane-per-block k_stream_out (MYYUV_STREAM_OUT).  Every test taking `codec`
-    runs on both."""
+    MYYUV_DECODER are read when the context is created).  Every test taking
+    `codec` runs on both."""
     import myyuv_hip
 
-    vals = {"MYYUV_ENCODER": request.param, "MYYUV_DECODER": request.param,
-            "MYYUV_STREAM_OUT": "coop" if request.param == "split" else "lane"}
+    vals = {"MYYUV_ENCODER": request.param, "MYYUV_DECODER": request.param}
     old = {k: os.environ.get(k) for k in vals}
     for k, v in vals.items():
         os.environ[k] = v

@@ -133,24 +133,6 @@ constexpr uint32_t kWideGrid = MYYUV_WIDE_GRID;  // workgroups of k_huff_encode_
 #endif
 constexpr uint32_t kR16Gate = MYYUV_R16_GATE;
 constexpr uint32_t kR16Grid = 4096;  // workgroups of k_huff_encode_r16 (grid-stride, 64 blocks each)
-// The CAP-16 tier sorts its list in windows of kR16Win entries by (distinct
-// symbols, message length) before encoding (MYYUV_R16_SORT, round 4): K2
-// records each listed block's key (min(n, 17) << 7 | msz, u16) beside the list
-// (r16_keys); a wave's heap loops run to its largest n and its position loops
-// to its longest message, so sorted waves do less work.
-#ifndef MYYUV_R16_SORT
-#define MYYUV_R16_SORT 1
-#endif
-constexpr uint32_t kR16Win = 1024;       // list entries per sorting window = threads per workgroup
-constexpr uint32_t kR16SortGrid = 256;   // workgroups (one resident per CU at 16 waves)
-// the keys of K2's list `work` (the list is `work`, the tier's rest list
-// work + nblk, the keys after both)
-__host__ __device__ __forceinline__ uint16_t* r16_keys(uint32_t* work, const FrameGeom& G) {
-  return reinterpret_cast<uint16_t*>(work + 2ull * G.nframes * G.cum[3]);
-}
-__host__ __device__ __forceinline__ uint32_t r16_key(uint32_t n, uint32_t msz) {
-  return ((n < 17u ? n : 17u) << 7) | msz;
-}
 #ifndef MYYUV_K2_GROUP
 #define MYYUV_K2_GROUP 256
 #endif

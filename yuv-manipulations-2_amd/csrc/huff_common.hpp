@@ -447,10 +447,7 @@ MYYUV_HD bool build_r(const CoefRegs& R, int msz, int wave_msz, EncState& S) {
       }
     }
   }
-  if (n > (uint32_t)CAP) {
-    S.n = n;  // (the distinct symbols: the overflow tier's sort key)
-    return false;
-  }
+  if (n > (uint32_t)CAP) return false;
   if (msz == 0) {  // all-zero block: one symbol 0, count 1 (Huffman.cpp:191-194)
     KP[0] = 0x800u;
     cnt = 1;

@@ -834,8 +834,7 @@ template <class Src>
 __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uint32_t T, uint32_t nloc,
                                             uint32_t* __restrict__ stage, uint32_t* __restrict__ tinfo,
                                             uint8_t* __restrict__ sizes, uint32_t* __restrict__ srcoff,
-                                            uint32_t* __restrict__ work, uint32_t* __restrict__ work_count,
-                                            uint16_t* __restrict__ wkey) {
+                                            uint32_t* __restrict__ work, uint32_t* __restrict__ work_count) {
   constexpr int kWaves = kTileWaves;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint32_t gb = src.gb;
@@ -943,11 +942,7 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(work_count, (uint32_t)__popcll(ovf));
     base = __builtin_amdgcn_readfirstlane(base);
-    if ((ovf >> lane) & 1) {
-      const uint32_t at = base + (uint32_t)__popcll(ovf & below);
-      work[at] = mg;
-      wkey[at] = (uint16_t)r16_key(S.n, (uint32_t)mm);
-    }
+    if ((ovf >> lane) & 1) work[base + (uint32_t)__popcll(ovf & below)] = mg;
   }
 #ifdef MYYUV_STAMPS
   if (lane == 0 && wid < 8192) g_k2_fstamps[wid * 8 + 7] = (uint32_t)(__builtin_amdgcn_s_memtime() - _w0);
@@ -1223,11 +1218,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
       uint32_t base = 0;
       if (ln == 0) base = atomicAdd(work_count, (uint32_t)__popcll(ovf));
       base = __builtin_amdgcn_readfirstlane(base);
-      if ((ovf >> ln) & 1) {
-        const uint32_t at = base + lanes_below(ovf);
-        work[at] = mg;
-        r16_keys(work, G)[at] = (uint16_t)r16_key(S.n, (uint32_t)mm);  // (the CAP-16 tier's sort key)
-      }
+      if ((ovf >> ln) & 1) work[base + lanes_below(ovf)] = mg;
     }
   }
   // ---- 4. the last wave out publishes the tiles' dense bytes
@@ -1360,7 +1351,7 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
   // ---- phase 2: K2 over the LDS image (its scratch over the transpose tiles)
   TileScratch& sc = *reinterpret_cast<TileScratch*>(&s_tile[0][0]);
   const LdsCoef src{s_img, s_rmk, coef, rmask, f * G.cum[3] + g0};
-  encode_tile(src, sc, T, nloc, stage, tinfo, sizes, srcoff, work, work_count, r16_keys(work, G));
+  encode_tile(src, sc, T, nloc, stage, tinfo, sizes, srcoff, work, work_count);
 }
 
 // Overflow pass (CAP=64), lane per block, for long worklists (noise-like
@@ -1414,103 +1405,6 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
 #ifndef MYYUV_R16_WAVES
 #define MYYUV_R16_WAVES 5  // waves per SIMD k_huff_encode_r16 is compiled for: 96 VGPRs, 8 spilled (3 waves at 131: -1.5 %, profiles/r3zzl_*)
 #endif
-namespace {
-// One listed block through the CAP-16 tier (lane per block): its chunk into
-// its overflow slot, or (more than 16 distinct symbols) onto work2.
-__device__ __forceinline__ void r16_block(const uint4* __restrict__ coef, const uint8_t* __restrict__ rmask,
-                                          const uint4* __restrict__ zq, const FrameGeom& G,
-                                          uint32_t* __restrict__ oslots, uint8_t* __restrict__ sizes,
-                                          uint32_t* __restrict__ tinfo, uint32_t* __restrict__ work2,
-                                          uint32_t* __restrict__ work2_count, bool live, uint32_t g) {
-  const uint32_t lane = threadIdx.x & 63u;
-  CoefRegs R;
-  R.load(coef, zq, g, live ? rmask[g] : 0u);
-  const int msz = live ? R.msz() : 0;
-  const int wmsz = max(wave_max(msz), 1);
-  EncState16 S;
-  const bool ok = live && build_r16(R, msz, wmsz, S);
-  if (ok) {
-    BitWriter bw;
-    bw.out = oslots + (size_t)g * kSlotWords;
-    emit_chunk16(S, wmsz, bw);
-    bw.align_byte();
-    bw.flush();
-    sizes[g] = (uint8_t)S.size;
-    atomicAdd(tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, S.size);  // the tile's overflow bytes
-  }
-  const uint64_t more = __ballot(live && !ok);
-  if (more) {
-    uint32_t b0 = 0;
-    if (lane == 0) b0 = atomicAdd(work2_count, (uint32_t)__popcll(more));
-    b0 = __builtin_amdgcn_readfirstlane(b0);
-    if ((more >> lane) & 1ull) work2[b0 + (uint32_t)__popcll(more & ((1ull << lane) - 1ull))] = g;
-  }
-}
-}  // namespace
-
-#if MYYUV_R16_SORT
-// Sorted form (round 4): one workgroup of kR16Win lanes per window of the
-// list.  The window's entries are counting-sorted in LDS by their K2 key —
-// distinct symbols (9 .. 16, more) major, message length in steps of 8 minor:
-// 81 buckets — so each wave holds blocks of one n and similar length; the
-// heap's push / pop loops run to the wave's largest n, the position loops to
-// its longest message.  Any key order is correct (it only permutes the
-// lanes): the keys are a schedule, not data.  On the bench frame's overflow
-// blocks a full sort cuts the tier's modelled work by 31 %, 1024-entry
-// windows by 26 % (n: 2,476 / 1,867 / 1,418 / 1,163 / 742 / 400 / 142 / 40
-// blocks with 9 .. 16 symbols, 14 more).
-constexpr uint32_t kR16Buckets = 9 * 9;  // (min(n, 17) - 9) x (msz >> 3), the dead slots after
-__device__ __forceinline__ uint32_t r16_bucket(uint32_t key) {
-  const uint32_t n = key >> 7, m = (key & 127u) >> 3;
-  return (n < 9u ? 0u : (n > 17u ? 8u : n - 9u)) * 9u + (m < 8u ? m : 8u);
-}
-__global__ __launch_bounds__(kR16Win) void k_huff_encode_r16(const uint4* __restrict__ coef,
-                                                        const uint8_t* __restrict__ rmask,
-                                                        const uint4* __restrict__ zq, FrameGeom G,
-                                                        uint32_t* __restrict__ oslots,
-                                                        uint8_t* __restrict__ sizes,
-                                                        uint32_t* __restrict__ tinfo,
-                                                        const uint32_t* __restrict__ work,
-                                                        const uint32_t* __restrict__ work_count,
-                                                        uint32_t* __restrict__ work2,
-                                                        uint32_t* __restrict__ work2_count) {
-  __shared__ uint32_t s_cnt[kR16Buckets + 1];
-  __shared__ uint32_t s_g[kR16Win];
-  const uint32_t cnt = *work_count;
-  if (cnt <= kR16Gate) return;  // one CAP-64 round takes the list
-  const uint32_t tid = threadIdx.x;
-  const uint16_t* keys = r16_keys(const_cast<uint32_t*>(work), G);
-  for (uint32_t base = blockIdx.x * kR16Win; base < cnt; base += gridDim.x * kR16Win) {
-    const uint32_t i = base + tid;
-    const bool live = i < cnt;
-    const uint32_t g = live ? work[i] : 0u;
-    const uint32_t b = live ? r16_bucket(keys[i]) : kR16Buckets;
-    if (tid <= kR16Buckets) s_cnt[tid] = 0;
-    __syncthreads();
-    const uint32_t r = atomicAdd(&s_cnt[b], 1u);  // rank inside the bucket (any order)
-    __syncthreads();
-    if (tid < 64) {  // exclusive scan of the 82 counts (two per lane)
-      const uint32_t c0 = 2 * tid < kR16Buckets + 1 ? s_cnt[2 * tid] : 0u;
-      const uint32_t c1 = 2 * tid + 1 < kR16Buckets + 1 ? s_cnt[2 * tid + 1] : 0u;
-      uint32_t incl = c0 + c1;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
-        if (tid >= (uint32_t)d) incl += o;
-      }
-      const uint32_t ex = incl - c0 - c1;
-      if (2 * tid < kR16Buckets + 1) s_cnt[2 * tid] = ex;
-      if (2 * tid + 1 < kR16Buckets + 1) s_cnt[2 * tid + 1] = ex + c0;
-    }
-    __syncthreads();
-    s_g[s_cnt[b] + r] = live ? g : ~0u;
-    __syncthreads();
-    const uint32_t gs = s_g[tid];
-    r16_block(coef, rmask, zq, G, oslots, sizes, tinfo, work2, work2_count, gs != ~0u, gs != ~0u ? gs : 0u);
-    __syncthreads();  // (the next window rewrites s_cnt / s_g)
-  }
-}
-#else
 __global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const uint4* __restrict__ coef,
                                                         const uint8_t* __restrict__ rmask,
                                                         const uint4* __restrict__ zq, FrameGeom G,
@@ -1523,12 +1417,34 @@ __global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const u
                                                         uint32_t* __restrict__ work2_count) {
   const uint32_t cnt = *work_count;
   if (cnt <= kR16Gate) return;  // one CAP-64 round takes the list
+  const uint32_t lane = threadIdx.x;
   for (uint32_t base = blockIdx.x * kWave; base < cnt; base += gridDim.x * kWave) {
-    const uint32_t i = base + threadIdx.x;
+    const uint32_t i = base + lane;
     const bool live = i < cnt;
-    r16_block(coef, rmask, zq, G, oslots, sizes, tinfo, work2, work2_count, live, live ? work[i] : 0u);
+    const uint32_t g = live ? work[i] : 0u;
+    CoefRegs R;
+    R.load(coef, zq, g, live ? rmask[g] : 0u);
+    const int msz = live ? R.msz() : 0;
+    const int wmsz = max(wave_max(msz), 1);
+    EncState16 S;
+    const bool ok = live && build_r16(R, msz, wmsz, S);
+    if (ok) {
+      BitWriter bw;
+      bw.out = oslots + (size_t)g * kSlotWords;
+      emit_chunk16(S, wmsz, bw);
+      bw.align_byte();
+      bw.flush();
+      sizes[g] = (uint8_t)S.size;
+      atomicAdd(tinfo + (size_t)tile_of_block(G, g) * kTInfoWords, S.size);  // the tile's overflow bytes
+    }
+    const uint64_t more = __ballot(live && !ok);
+    if (more) {
+      uint32_t b0 = 0;
+      if (lane == 0) b0 = atomicAdd(work2_count, (uint32_t)__popcll(more));
+      b0 = __builtin_amdgcn_readfirstlane(b0);
+      if ((more >> lane) & 1ull) work2[b0 + (uint32_t)__popcll(more & ((1ull << lane) - 1ull))] = g;
+    }
   }
 }
-#endif
 
 }  // namespace myyuv_gpu

@@ -334,176 +334,4 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
   }
 }
 
-// The same tile -> stream step with the copy split by output dwords instead of
-// by chunks (round 4): lane-per-block k_stream_out runs every lane's copy loop
-// to the longest chunk of its wave, a few long chunks among many 7-byte ones,
-// and its waves hold their slots for it (12.9 % of all wave-cycles for 6.2 %
-// of the VALU work, profiles/r3zb_sq_counters.txt).  Here the chunks'
-// offsets and sources go to LDS (one load round trip: size and srcoff), then
-// the workgroup walks the tile's output dwords, 256 at a time, lane i taking
-// dwords i, i + 256, ...:
-//   * the chunk holding a dword's first byte: every chunk marks the dword
-//     holding its own first byte (chunks are >= 7 bytes, so at most one starts
-//     in any dword), a workgroup max-scan over the marks gives each dword the
-//     last chunk starting at or before it, and one offset compare settles a
-//     chunk starting mid-dword;
-//   * the dword: two source words of that chunk, funnel-shifted; bytes past
-//     the chunk's end are the next chunk's first (its header, <= 3 bytes),
-//     whose source words are loaded in the same round trip.
-// Ownership rules as k_stream_out: the dword holding the tile's first byte
-// belongs to the previous tile (completed there with this tile's first
-// header), except at a plane's first chunk (byte stores: it meets the size
-// array); a plane's last dword is written with byte stores (it meets the next
-// plane's header).  Dwords are claimed in rounds of kCoopRound (one round for
-// a 4032x3008 q=50 tile, ~3 KB).  The rules were checked on 3,000 random
-// tile sequences by a host model before the kernel was written: every byte
-// written exactly once, with its chunk's value.
-namespace {
-constexpr uint32_t kCoopRound = 1024;  // output dwords per round (4 per lane)
-}
-
-__global__ __launch_bounds__(256) void k_stream_out_coop(const uint32_t* __restrict__ stage,
-                                                         const uint32_t* __restrict__ tinfo,
-                                                         const uint8_t* __restrict__ sizes,
-                                                         const uint32_t* __restrict__ srcoff,
-                                                         const uint32_t* __restrict__ oslots, FrameGeom G,
-                                                         uint8_t* __restrict__ out, uint32_t cap) {
-  __shared__ uint32_t s_off[kK2Group + 1];  // tile-local byte offset of chunk c (block order); [nloc] = total
-  __shared__ uint32_t s_so[kK2Group + 1];   // srcoff of chunk c; [nloc]: the next tile's first block's
-  __shared__ uint32_t s_mark[kCoopRound];   // per dword of the round: last chunk (+1) starting at or before it
-  __shared__ uint32_t s_w[4], s_carry;
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t t = blockIdx.x, f = blockIdx.y, ntile = G.tcum[3];
-  const uint32_t T = f * ntile + t;
-  const int p = tile_plane(G, t);
-  const uint32_t g0 = tile_first(G, p, t);
-  const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
-  const uint32_t gb = f * G.cum[3] + g0;
-  out += (size_t)f * cap;
-  const uint32_t x = tinfo[(size_t)T * kTInfoWords + kTInfoPrefix];  // the tile's content prefix
-  const uint32_t ppre = tinfo[((size_t)f * ntile + G.tcum[p]) * kTInfoWords + kTInfoPrefix];
-  const bool plane_end = g0 + nloc == G.cum[p + 1];
-  const bool plane_first = g0 == G.cum[p];
-  // chunk c's source words and byte shift (c == nloc: the next tile's first chunk)
-  auto chunk_src = [&](uint32_t c, uint32_t so, uint32_t& sh) -> const uint32_t* {
-    if (so == kSrcOverflow) {
-      sh = 0;
-      return oslots + (size_t)(gb + c) * kSlotWords;
-    }
-    sh = so & 3u;
-    return stage + (size_t)win_first_tile(c < nloc ? T : T + 1) * (kTileCap / 4) + (so >> 2);
-  };
-  // the first 4 bytes at a chunk's start (its header): two source words
-  auto head_of = [&](uint32_t c) -> uint32_t {
-    uint32_t sh;
-    const uint32_t* s1 = chunk_src(c, s_so[c], sh);
-    const uint32_t a = s1[0], b = s1[1];
-    return sh ? (a >> (8 * sh)) | (b << (32 - 8 * sh)) : a;
-  };
-  // ---- phase 1, lane per block: size, source, offsets (one load round trip)
-  const bool live = tid < nloc;
-  const uint32_t sz = live ? sizes[gb + tid] : 0u;
-  const uint32_t so = live ? srcoff[gb + tid] : 0u;
-  const uint32_t so_next = (tid == nloc - 1 && !plane_end) ? srcoff[gb + nloc] : 0u;
-  const uint32_t incl = wave_inclusive_scan(sz);
-  if (lane == 63) s_w[wave] = incl;
-  __syncthreads();
-  uint32_t o = incl - sz;
-#pragma unroll
-  for (uint32_t w = 0; w < 4; w++) o += w < wave ? s_w[w] : 0u;
-  const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-  if (live) {
-    s_off[tid] = o;
-    s_so[tid] = so;
-  }
-  if (tid == nloc - 1) {
-    s_off[nloc] = tot;
-    s_so[nloc] = so_next;
-  }
-  // ---- chunk_size[] bytes (DCTYUVPlane layout: after the plane's 8-byte header)
-  const uint64_t spos = 12ull + 8ull * (p + 1) + ppre + g0;
-  if (live && spos + tid < cap) out[spos + tid] = (uint8_t)sz;
-  if (tot == 0) return;  // (no live block: uniform)
-  const uint64_t P0 = 12ull + 8ull * (p + 1) + G.cum[p + 1] + x;  // the tile's first content byte
-  const uint64_t D0 = (P0 + 3) >> 2;                              // the first dword the tile owns
-  const uint32_t J = (uint32_t)(((P0 + tot - 1) >> 2) - D0 + 1);  // dwords the tile owns
-  const uint32_t lead = (uint32_t)(4 * D0 - P0);                  // chunk 0's bytes before dword D0
-  // chunk tid's first dword, relative to D0 (chunk 0 marks dword 0)
-  const uint32_t jc = live ? (tid == 0 ? 0u : (uint32_t)(((P0 + o) >> 2) - D0)) : ~0u;
-  if (tid == 0) s_carry = 0;
-  __syncthreads();  // (s_off / s_so complete)
-  if (plane_first && lead && tid == 0) {  // the dword before is shared with the size array
-    const uint32_t h = head_of(0);
-    for (uint32_t k = 0; k < lead; k++)
-      if (P0 + k < cap) out[P0 + k] = (uint8_t)(h >> (8 * k));
-  }
-  for (uint32_t R = 0; R < J; R += kCoopRound) {
-    // ---- marks, then a workgroup max-scan (4 per lane)
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) s_mark[4 * tid + k] = 0;
-    __syncthreads();
-    if (jc >= R && jc < R + kCoopRound) s_mark[jc - R] = tid + 1;
-    __syncthreads();
-    uint32_t m[4], mx = s_carry;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      mx = max(mx, s_mark[4 * tid + k]);
-      m[k] = mx;
-    }
-    uint32_t wm = mx;  // inclusive max over the wave's lanes
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t v = (uint32_t)__shfl_up((int)wm, d, 64);
-      if (lane >= (uint32_t)d) wm = max(wm, v);
-    }
-    const uint32_t before = (uint32_t)__shfl_up((int)wm, 1, 64);
-    __syncthreads();  // (every lane has read the carry and the marks)
-    if (lane == 63) s_w[wave] = wm;
-    __syncthreads();
-    uint32_t pm = lane ? before : 0u;
-#pragma unroll
-    for (uint32_t w = 0; w < 4; w++) pm = w < wave ? max(pm, s_w[w]) : pm;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) s_mark[4 * tid + k] = max(pm, m[k]);
-    __syncthreads();
-    if (tid == 0) s_carry = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
-    // ---- the round's dwords: lane tid takes R + tid + 256 k; the source
-    // words of its chunk and, when the dword runs past the chunk, of the
-    // next chunk's header are loaded together (one round trip)
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      const uint32_t j = R + tid + 256u * k;
-      if (j >= J) break;
-      const uint64_t D = D0 + j;
-      const uint32_t b = (uint32_t)(4 * D - P0);  // tile-local byte at the dword's start
-      uint32_t c = s_mark[j - R] - 1u;
-      uint32_t oc = s_off[c];
-      if (oc > b) {  // chunk c starts inside the dword: its first byte is chunk c - 1's
-        c--;
-        oc = s_off[c];
-      }
-      const uint32_t avail = s_off[c + 1] - b;  // chunk c's bytes from the dword's start
-      uint32_t sh;
-      const uint32_t* src = chunk_src(c, s_so[c], sh);
-      const uint32_t r = sh + (b - oc), wi = r >> 2, q = r & 3u;
-      const uint32_t a0 = src[wi], a1 = src[wi + 1];  // (buffers padded: wi + 1 stays inside)
-      const bool more = avail < 4 && (c + 1 < nloc || !plane_end);
-      const uint32_t hn = more ? head_of(c + 1) : 0u;
-      uint32_t v = q ? (a0 >> (8 * q)) | (a1 << (32 - 8 * q)) : a0;
-      const uint64_t pos = 4 * D;
-      if (avail < 4) {
-        if (more) {
-          v = (v & ((1u << (8 * avail)) - 1u)) | (hn << (8 * avail));
-        } else {  // the plane's last bytes: the next plane's header follows
-          for (uint32_t i = 0; i < avail; i++)
-            if (pos + i < cap) out[pos + i] = (uint8_t)(v >> (8 * i));
-          continue;
-        }
-      }
-      if (pos + 4 <= cap) *reinterpret_cast<uint32_t*>(out + pos) = v;
-    }
-    __syncthreads();  // (the next round rewrites the marks)
-  }
-}
-
 }  // namespace myyuv_gpu

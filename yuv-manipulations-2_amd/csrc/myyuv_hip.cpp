@@ -51,8 +51,6 @@ __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*,
                              uint32_t, unsigned long long*);
 __global__ void k_stream_out(const uint32_t*, const uint32_t*, const uint8_t*, const uint32_t*,
                              const uint32_t*, FrameGeom, uint8_t*, uint32_t);
-__global__ void k_stream_out_coop(const uint32_t*, const uint32_t*, const uint8_t*, const uint32_t*,
-                                  const uint32_t*, FrameGeom, uint8_t*, uint32_t);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
                               uint4*, uint8_t*, unsigned long long*);
@@ -196,9 +194,6 @@ struct myyuv_hip_ctx {
   // decoder: the fused k_decode_idct (default), or K5 -> K6 through HBM
   // (MYYUV_DECODER=split)
   bool fused_dec = true;
-  // stream writer: k_stream_out_coop (copy split by output dwords) or the
-  // lane-per-block k_stream_out (MYYUV_STREAM_OUT=coop|lane)
-  bool coop_out = true;
   // chained scan (k_chain.hpp): per-tile status words tagged with the launch
   // epoch, counted here
   DevBuf status;
@@ -324,9 +319,8 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   const uint32_t ntiles = ceil_div(G.cum[3], kScanTile);
   int e = 0;
   e |= c->coef.grow((size_t)nwaves * kCoefQuadsPerWave * 16);  // natural-order quads
-  // (+64 B: the stream writers read a word past a chunk's last one)
-  e |= c->stage.grow((size_t)win_tiles_alloc(nf * G.tcum[3]) * kTileCap + 64);
-  e |= c->oslots.grow((size_t)nblk * kMaxChunk + 64);
+  e |= c->stage.grow((size_t)win_tiles_alloc(nf * G.tcum[3]) * kTileCap);
+  e |= c->oslots.grow((size_t)nblk * kMaxChunk);
   e |= c->tinfo.grow((size_t)nf * G.tcum[3] * kTInfoWords * 4);
   e |= c->srcoff.grow((size_t)nblk * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
@@ -342,8 +336,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->psize.grow(4);
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
   // [0], [1]: overflow counts, then K2's list and (single frames) the CAP-16 tier's (launch_overflow)
-  // (then the CAP-16 tier's rest list, nblk words, and the u16 sort keys of K2's list: r16_keys)
-  e |= c->work.grow((size_t)nblk * 10 + 256);
+  e |= c->work.grow((size_t)nblk * (nf == 1 || MYYUV_R16_BATCH ? 8 : 4) + 256);
   const size_t st_bytes = (size_t)nf * (ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
@@ -401,12 +394,8 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
     // work[1], the tier's count (its own node: a store in K1's prologue
     // shifted K1's loop and cost it 5 %, profiles/r3zx_*)
     e |= hipMemsetAsync(count2, 0, 4, s) != hipSuccess;
-#if MYYUV_R16_SORT
-    const uint32_t r16 = std::min(ceil_div(nblk, kR16Win), kR16SortGrid), r16_block = kR16Win;
-#else
-    const uint32_t r16 = ceil_div(nblk, kWave) < kR16Grid ? ceil_div(nblk, kWave) : kR16Grid, r16_block = kWave;
-#endif
-    e |= launch(c, MYYUV_K_HUFF_R16, k_huff_encode_r16, dim3(r16), dim3(r16_block), s, c->coef.as<const uint4>(),
+    const uint32_t r16 = ceil_div(nblk, kWave) < kR16Grid ? ceil_div(nblk, kWave) : kR16Grid;
+    e |= launch(c, MYYUV_K_HUFF_R16, k_huff_encode_r16, dim3(r16), dim3(kWave), s, c->coef.as<const uint4>(),
                 c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G, c->oslots.as<uint32_t>(),
                 c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
                 list2, count2);
@@ -451,7 +440,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   }
   e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(256), s, c->tinfo.as<uint32_t>(), G,
               static_cast<uint8_t*>(d_out), cap, d_size, err);
-  e |= launch(c, MYYUV_K_COMPACT, c->coop_out ? k_stream_out_coop : k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
+  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
               c->stage.as<const uint32_t>(), c->tinfo.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
               c->srcoff.as<const uint32_t>(), c->oslots.as<const uint32_t>(), G, static_cast<uint8_t*>(d_out),
               cap);
@@ -623,8 +612,6 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
         c->fused = v && std::strcmp(v, "fused") == 0;
         const char* d = std::getenv("MYYUV_DECODER");
         c->fused_dec = !(d && std::strcmp(d, "split") == 0);
-        const char* so = std::getenv("MYYUV_STREAM_OUT");
-        c->coop_out = !(so && std::strcmp(so, "lane") == 0);
       }
       // tuning knobs (diagnostic; default 100): K1 / K6 grids as a percentage
       // of the resident workgroups, leaving wave slots to other launch groups
