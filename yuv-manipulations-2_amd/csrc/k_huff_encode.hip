@@ -997,16 +997,6 @@ __device__ __forceinline__ int wave_max_ln(int v, uint32_t ln) {
   return v;
 }
 
-// The nonzero coefficient rows of the non-single classes kept in LDS at
-// classification (MYYUV_K2_CACHE_KB; 0 = off): a run whose blocks are kept
-// reads them from LDS instead of reloading them from HBM / L2 in its sorted,
-// scattered order.  Each wave keeps its own blocks in its quarter of the
-// cache, first come first kept; a block that does not fit is reloaded.
-#ifndef MYYUV_K2_CACHE_KB
-#define MYYUV_K2_CACHE_KB 0
-#endif
-constexpr uint32_t kK2CacheQuads = MYYUV_K2_CACHE_KB * 64u;  // 16-B rows
-constexpr uint32_t kK2CacheWave = kK2CacheQuads / kTileWaves;
 #ifndef MYYUV_K2_DC_LDS
 #define MYYUV_K2_DC_LDS 1  // single-class runs take the DC from LDS (kept at classification), not from HBM
 #endif
@@ -1015,41 +1005,12 @@ struct WinScratch {
 #if MYYUV_K2_DC_LDS
   uint16_t dc[kWinBlocks];    // window slot -> its DC coefficient (word 0 of quad 0)
 #endif
-#if MYYUV_K2_CACHE_KB > 0
-  uint16_t coff[kWinBlocks];  // window slot -> first quad of its nonzero rows in `cache`, 0xFFFF: not kept
-  uint4 cache[kK2CacheQuads];  // nonzero coefficient rows kept at classification (four per-wave regions)
-#endif
   uint8_t msz[kWinBlocks], cls[kWinBlocks], rm[kWinBlocks];
   uint32_t cnt[kScanVals];    // per (key, sort slot): count, then exclusive position
   uint32_t gb[kWinTiles];     // batch-global index of tile k's block 0
   uint32_t tot[kWinTiles];    // tile k's dense chunk bytes
   uint32_t next, done, ntl;   // run counter, finished waves, the window's tiles
 };
-
-// A run lane's block: its nonzero rows from the LDS cache when they were kept
-// at classification, else from HBM / L2 (masked-off rows from the zero buffer)
-__device__ __forceinline__ void run_load(CoefRegs& R, const WinScratch& sc, const uint4* __restrict__ coef,
-                                         const uint4* __restrict__ zq, bool live, uint32_t sl, uint32_t mg,
-                                         uint32_t mrm) {
-#if MYYUV_K2_CACHE_KB > 0
-  const uint32_t co = live ? sc.coff[sl] : 0xFFFFu;
-  if (co != 0xFFFFu) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const bool nz = (mrm >> c) & 1u;
-      const uint4 v = nz ? sc.cache[co + r] : make_uint4(0u, 0u, 0u, 0u);
-      r += nz ? 1u : 0u;
-      R.w[4 * c] = v.x;
-      R.w[4 * c + 1] = v.y;
-      R.w[4 * c + 2] = v.z;
-      R.w[4 * c + 3] = v.w;
-    }
-    return;
-  }
-#endif
-  R.load(coef, zq, live ? mg : 0u, live ? mrm : 0u);
-}
 
 }  // namespace
 
@@ -1122,9 +1083,6 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
 #pragma unroll
   for (uint32_t k = 0; k < kWinTiles; k++) rmv[k] = tid < nlk[k] ? rmask[gbk[k] + tid] : 0u;
   // round k + 1's coefficients are loaded before round k is classified
-#if MYYUV_K2_CACHE_KB > 0
-  uint32_t ctop = 0;  // quads taken in this wave's cache region (uniform)
-#endif
   CoefRegs RR[2];
   RR[0].load(coef, zq, tid < nlk[0] ? gbk[0] + tid : 0u, rmv[0]);
 #pragma unroll
@@ -1142,34 +1100,6 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     const uint32_t key = sort_key(cls, m);
 #if MYYUV_K2_DC_LDS
     sc.dc[(k << 8) | tid] = (uint16_t)RR[k & 1].w[0];  // (masked rows were loaded as zeros)
-#endif
-#if MYYUV_K2_CACHE_KB > 0
-    {
-      // keep the block's nonzero rows in this wave's cache region if they fit
-      const bool want = cls != kClassDead && cls != kClassSingle;
-      const uint32_t nr = want ? (uint32_t)__popc(rm) : 0u;
-      uint32_t incl = nr;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
-        if (lane >= (uint32_t)d) incl += o;
-      }
-      const uint32_t off = ctop + incl - nr;
-      const bool keep = want && off + nr <= kK2CacheWave;
-      sc.coff[(k << 8) | tid] = keep ? (uint16_t)(wave * kK2CacheWave + off) : (uint16_t)0xFFFFu;
-      if (keep) {
-        uint4* dst = sc.cache + wave * kK2CacheWave + off;
-        uint32_t r = 0;
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-          if ((rm >> c) & 1u) {
-            dst[r] = make_uint4(RR[k & 1].w[4 * c], RR[k & 1].w[4 * c + 1], RR[k & 1].w[4 * c + 2], RR[k & 1].w[4 * c + 3]);
-            r++;
-          }
-        }
-      }
-      ctop += (uint32_t)__shfl((int)incl, 63, 64);
-    }
 #endif
     uint32_t rk = 0;
 #pragma unroll
@@ -1263,11 +1193,11 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
       }
     } else if (wcls == kClassR4) {
       CoefRegs R;
-      run_load(R, sc, coef, zq, live, sl, mg, mrm);
+      R.load(coef, zq, live ? mg : 0u, live ? mrm : 0u);
       if (live) ok = build_r<4>(R, mm, wmsz, S);
     } else {
       CoefRegs R;
-      run_load(R, sc, coef, zq, live, sl, mg, mrm);
+      R.load(coef, zq, live ? mg : 0u, live ? mrm : 0u);
       if (live) ok = build_r<8>(R, mm, wmsz, S);
     }
     // the run's chunks back to back (offsets by a wave scan of the sizes),

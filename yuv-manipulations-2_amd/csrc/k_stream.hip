@@ -216,164 +216,120 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
   }
 }
 
-// kK4Tiles tiles per workgroup: each tile's chunks, in block order, from the
-// K2 runs / overflow slots straight into the stream, one lane per block of
-// each tile.  Every stream dword inside a plane's content is stored once, by
-// the chunk owning its first byte, with the next chunk's first bytes — at
-// most 3, so always the next chunk's header (u16 nbits, u8 table_bytes),
-// which the next lane loads anyway — completing its last dword.  Only where
-// the content meets other data (a plane's size array before its first chunk,
-// the next plane's header after its last) are the shared dwords written with
-// byte stores.  No LDS image, no atomics.  The workgroup's tiles are
-// independent; they share a workgroup so that their loads are in flight
-// together: the kernel is two dependent load round trips (sizes / srcoff,
-// then the chunk words) per tile, and with one tile per workgroup its waves
-// spent 0.61 of their cycles waiting (13.6 % of all wave-cycles of the
-// pipeline for 6.9 % of its VALU work, profiles/r4b_sq_counters.txt).
+// One tile: its chunks, in block order, from the K2 runs / overflow slots
+// straight into the stream, one lane per block.  Every stream dword inside a
+// plane's content is stored once, by the chunk owning its first byte, with
+// the next chunk's first bytes — at most 3, so always the next chunk's header
+// (u16 nbits, u8 table_bytes), which the next lane loads anyway — completing
+// its last dword.  Only where the content meets other data (a plane's size
+// array before its first chunk, the next plane's header after its last) are
+// the shared dwords written with byte stores.  No LDS image, no atomics.
 __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__ stage,
                                                     const uint32_t* __restrict__ tinfo,
                                                     const uint8_t* __restrict__ sizes,
                                                     const uint32_t* __restrict__ srcoff,
                                                     const uint32_t* __restrict__ oslots, FrameGeom G,
                                                     uint8_t* __restrict__ out, uint32_t cap) {
-  __shared__ uint32_t s_wt[kK4Tiles][4], s_hdr[kK4Tiles][4];
+  __shared__ uint32_t s_wt[4], s_hdr[4];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t f = blockIdx.y, ntile = G.tcum[3];
+  const uint32_t t = blockIdx.x, f = blockIdx.y, ntile = G.tcum[3];
+  const uint32_t T = f * ntile + t;
+  const int p = tile_plane(G, t);
+  const uint32_t g0 = tile_first(G, p, t);
+  const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
+  const uint32_t gb = f * G.cum[3] + g0;
   out += (size_t)f * cap;
-  uint32_t sz[kK4Tiles], sh[kK4Tiles], nsrc[kK4Tiles], hdr[kK4Tiles], nxh[kK4Tiles];
-  const uint32_t* src[kK4Tiles];
-  uint32_t v[kK4Tiles][9];
-  // ---- every tile's sizes and sources, then every tile's first chunk words:
-  // the loads of all the workgroup's tiles in flight together
-#pragma unroll
-  for (uint32_t j = 0; j < kK4Tiles; j++) {
-    const uint32_t t = blockIdx.x * kK4Tiles + j;
-    const bool tv = t < ntile;
-    const int p = tile_plane(G, tv ? t : 0u);
-    const uint32_t g0 = tile_first(G, p, tv ? t : 0u);
-    const uint32_t nloc = tv ? min(kK2Group, G.cum[p + 1] - g0) : 0u;
-    const uint32_t gb = f * G.cum[3] + g0;
-    const bool live = tid < nloc;
-    sz[j] = live ? sizes[gb + tid] : 0u;
-    const uint32_t so = live ? srcoff[gb + tid] : 0u;
-    if (so == kSrcOverflow) {
-      src[j] = oslots + (size_t)(gb + tid) * kSlotWords;
-      sh[j] = 0;
-    } else {
-      src[j] = stage + (size_t)win_first_tile(f * ntile + t) * (kTileCap / 4) + (so >> 2);  // (window-relative)
-      sh[j] = so & 3u;
-    }
+  const uint32_t x = tinfo[(size_t)T * kTInfoWords + kTInfoPrefix];  // the tile's content prefix
+  const uint32_t ppre = tinfo[((size_t)f * ntile + G.tcum[p]) * kTInfoWords + kTInfoPrefix];
+  // the lane's block, and for the tile's last block the next tile's first
+  // (its header completes the last dword when the plane goes on)
+  const bool live = tid < nloc;
+  const bool plane_end = g0 + nloc == G.cum[p + 1];
+  const uint32_t sz = live ? sizes[gb + tid] : 0u;
+  const uint32_t so = live ? srcoff[gb + tid] : 0u;
+  const uint32_t* src;
+  uint32_t sh;  // source byte misalignment
+  if (so == kSrcOverflow) {
+    src = oslots + (size_t)(gb + tid) * kSlotWords;
+    sh = 0;
+  } else {
+    src = stage + (size_t)win_first_tile(T) * (kTileCap / 4) + (so >> 2);  // (window-relative)
+    sh = so & 3u;
   }
-#pragma unroll
-  for (uint32_t j = 0; j < kK4Tiles; j++) {
-    // source words 8 (+1) per load round trip; the first round also gives the
-    // chunk's header
-    nsrc[j] = (sh[j] + sz[j] + 3) >> 2;
-#pragma unroll
-    for (uint32_t k = 0; k < 9; k++) v[j][k] = (k < nsrc[j]) ? src[j][k] : 0u;
+  uint32_t nxh = 0;  // the next tile's first header (lane nloc - 1, plane going on)
+  if (tid == nloc - 1 && !plane_end) {
+    const uint32_t so1 = srcoff[gb + nloc];
+    const uint32_t* s1 = so1 == kSrcOverflow ? oslots + (size_t)(gb + nloc) * kSlotWords
+                                             : stage + (size_t)win_first_tile(T + 1) * (kTileCap / 4) + (so1 >> 2);
+    const uint32_t r1 = so1 == kSrcOverflow ? 0u : so1 & 3u;
+    nxh = r1 ? (s1[0] >> (8 * r1)) | (s1[1] << (32 - 8 * r1)) : s1[0];
   }
+  // source words 8 (+1) per load round trip; the first round also gives the
+  // chunk's header
+  const uint32_t nsrc = (sh + sz + 3) >> 2;
+  uint32_t v[9];
 #pragma unroll
-  for (uint32_t j = 0; j < kK4Tiles; j++) {
-    // the next tile's first header (lane nloc - 1, the plane going on)
-    const uint32_t t = blockIdx.x * kK4Tiles + j;
-    const bool tv = t < ntile;
-    const int p = tile_plane(G, tv ? t : 0u);
-    const uint32_t g0 = tile_first(G, p, tv ? t : 0u);
-    const uint32_t nloc = tv ? min(kK2Group, G.cum[p + 1] - g0) : 0u;
-    const uint32_t gb = f * G.cum[3] + g0;
-    const bool plane_end = g0 + nloc == G.cum[p + 1];
-    nxh[j] = 0;
-    if (tv && tid == nloc - 1 && !plane_end) {
-      const uint32_t T1 = f * ntile + t + 1;
-      const uint32_t so1 = srcoff[gb + nloc];
-      const uint32_t* s1 = so1 == kSrcOverflow ? oslots + (size_t)(gb + nloc) * kSlotWords
-                                               : stage + (size_t)win_first_tile(T1) * (kTileCap / 4) + (so1 >> 2);
-      const uint32_t r1 = so1 == kSrcOverflow ? 0u : so1 & 3u;
-      nxh[j] = r1 ? (s1[0] >> (8 * r1)) | (s1[1] << (32 - 8 * r1)) : s1[0];
-    }
-  }
-  // ---- offsets in each tile (block order), the next lane's header
-  uint32_t incl[kK4Tiles];
-#pragma unroll
-  for (uint32_t j = 0; j < kK4Tiles; j++) {
-    hdr[j] = sh[j] ? (v[j][0] >> (8 * sh[j])) | (v[j][1] << (32 - 8 * sh[j])) : v[j][0];
-    incl[j] = wave_inclusive_scan(sz[j]);
-    if (lane == 63) s_wt[j][wave] = incl[j];
-    if (lane == 0) s_hdr[j][wave] = hdr[j];
-  }
+  for (uint32_t k = 0; k < 9; k++) v[k] = (k < nsrc) ? src[k] : 0u;
+  const uint32_t hdr = sh ? (v[0] >> (8 * sh)) | (v[1] << (32 - 8 * sh)) : v[0];
+  // ---- offsets in the tile (block order), the next lane's header
+  const uint32_t incl = wave_inclusive_scan(sz);
+  if (lane == 63) s_wt[wave] = incl;
+  if (lane == 0) s_hdr[wave] = hdr;
   __syncthreads();
+  uint32_t o = incl - sz;
 #pragma unroll
-  for (uint32_t j = 0; j < kK4Tiles; j++) {
-    const uint32_t t = blockIdx.x * kK4Tiles + j;
-    if (t >= ntile) break;  // (uniform)
-    const uint32_t T = f * ntile + t;
-    const int p = tile_plane(G, t);
-    const uint32_t g0 = tile_first(G, p, t);
-    const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
-    const uint32_t x = tinfo[(size_t)T * kTInfoWords + kTInfoPrefix];  // the tile's content prefix
-    const uint32_t ppre = tinfo[((size_t)f * ntile + G.tcum[p]) * kTInfoWords + kTInfoPrefix];
-    const bool live = tid < nloc;
-    const bool plane_end = g0 + nloc == G.cum[p + 1];
-    const uint32_t szj = sz[j], shj = sh[j];
-    uint32_t o = incl[j] - szj;
+  for (uint32_t w = 0; w < 4; w++) o += w < wave ? s_wt[w] : 0u;
+  uint32_t nh = (uint32_t)__shfl_down((int)hdr, 1, 64);
+  if (lane == 63) nh = wave < 3 ? s_hdr[wave + 1] : 0u;
+  if (tid == nloc - 1) nh = nxh;
+  const bool has_next = tid + 1 < nloc || !plane_end;  // a chunk follows in this plane
+  // ---- chunk_size[] bytes (DCTYUVPlane layout: after the plane's 8-byte header)
+  const uint64_t spos = 12ull + 8ull * (p + 1) + ppre + g0;
+  if (live && spos + tid < cap) out[spos + tid] = (uint8_t)sz;
+  if (!live || sz == 0) return;
+  const uint64_t P = 12ull + 8ull * (p + 1) + G.cum[p + 1] + x + o;  // the chunk's stream position
+  if (P + sz > cap) return;  // (capacity: k_tile_scan reports it)
+  // ---- chunk bytes k .. k+3 (from source byte sh + k), the next header after byte sz
+  auto word_at = [&](uint32_t k, const uint32_t* w, uint32_t j0) -> uint32_t {
+    const uint32_t r = sh + k, i = (r >> 2) - j0, q = r & 3u;
+    return q ? (w[i] >> (8 * q)) | (w[i + 1] << (32 - 8 * q)) : w[i];
+  };
+  const uint32_t lead = (uint32_t)((4u - (uint32_t)(P & 3u)) & 3u);  // chunk bytes before the first own dword
+  const bool plane_first = g0 + tid == G.cum[p];
+  if (plane_first && lead) {  // the dword before is shared with the size array
+    const uint32_t w = word_at(0, v, 0);
+    for (uint32_t k = 0; k < lead; k++) out[P + k] = (uint8_t)(w >> (8 * k));
+  }
+  uint32_t j0 = 0;  // first source word held in v
+  uint32_t k = lead;
+  // 16 chunk bytes per store while 16 remain (the wave's loop runs to its
+  // longest chunk: a quarter of the iterations of dword stores)
+  for (; k + 16u <= sz; k += 16u) {
+    const uint32_t need = (sh + k) >> 2;
+    if (need + 4 >= j0 + 9) {  // refill
+      j0 = need;
 #pragma unroll
-    for (uint32_t w = 0; w < 4; w++) o += w < wave ? s_wt[j][w] : 0u;
-    uint32_t nh = (uint32_t)__shfl_down((int)hdr[j], 1, 64);
-    if (lane == 63) nh = wave < 3 ? s_hdr[j][wave + 1] : 0u;
-    if (tid == nloc - 1) nh = nxh[j];
-    const bool has_next = tid + 1 < nloc || !plane_end;  // a chunk follows in this plane
-    // ---- chunk_size[] bytes (DCTYUVPlane layout: after the plane's 8-byte header)
-    const uint64_t spos = 12ull + 8ull * (p + 1) + ppre + g0;
-    if (live && spos + tid < cap) out[spos + tid] = (uint8_t)szj;
-    if (!live || szj == 0) continue;
-    const uint64_t P = 12ull + 8ull * (p + 1) + G.cum[p + 1] + x + o;  // the chunk's stream position
-    if (P + szj > cap) continue;  // (capacity: k_tile_scan reports it)
-    // ---- chunk bytes k .. k+3 (from source byte sh + k), the next header after byte sz
-    const uint32_t* sj = src[j];
-    uint32_t vj[9];  // (a tile-local copy: indexed dynamically below, it stays in registers)
-#pragma unroll
-    for (uint32_t i = 0; i < 9; i++) vj[i] = v[j][i];
-    auto word_at = [&](uint32_t k, const uint32_t* w, uint32_t j0) -> uint32_t {
-      const uint32_t r = shj + k, i = (r >> 2) - j0, q = r & 3u;
-      return q ? (w[i] >> (8 * q)) | (w[i + 1] << (32 - 8 * q)) : w[i];
-    };
-    const uint32_t lead = (uint32_t)((4u - (uint32_t)(P & 3u)) & 3u);  // chunk bytes before the first own dword
-    const bool plane_first = g0 + tid == G.cum[p];
-    if (plane_first && lead) {  // the dword before is shared with the size array
-      const uint32_t w = word_at(0, vj, 0);
-      for (uint32_t k = 0; k < lead; k++) out[P + k] = (uint8_t)(w >> (8 * k));
+      for (uint32_t i = 0; i < 9; i++) v[i] = (j0 + i < nsrc) ? src[j0 + i] : 0u;
     }
-    uint32_t j0 = 0;  // first source word held in v
-    uint32_t k = lead;
-    // 16 chunk bytes per store while 16 remain (the wave's loop runs to its
-    // longest chunk: a quarter of the iterations of dword stores)
-    for (; k + 16u <= szj; k += 16u) {
-      const uint32_t need = (shj + k) >> 2;
-      if (need + 4 >= j0 + 9) {  // refill
-        j0 = need;
+    const Dw4 o{word_at(k, v, j0), word_at(k + 4, v, j0), word_at(k + 8, v, j0), word_at(k + 12, v, j0)};
+    *reinterpret_cast<Dw4*>(out + P + k) = o;  // (4-byte aligned: P + lead is)
+  }
+  for (; k < sz; k += 4) {
+    const uint32_t need = (sh + k) >> 2;
+    if (need + 1 >= j0 + 9) {  // refill (chunks over ~28 bytes)
+      j0 = need;
 #pragma unroll
-        for (uint32_t i = 0; i < 9; i++) vj[i] = (j0 + i < nsrc[j]) ? sj[j0 + i] : 0u;
-      }
-      const Dw4 ow{word_at(k, vj, j0), word_at(k + 4, vj, j0), word_at(k + 8, vj, j0), word_at(k + 12, vj, j0)};
-      *reinterpret_cast<Dw4*>(out + P + k) = ow;  // (4-byte aligned: P + lead is)
+      for (uint32_t i = 0; i < 9; i++) v[i] = (j0 + i < nsrc) ? src[j0 + i] : 0u;
     }
-    for (; k < szj; k += 4) {
-      const uint32_t need = (shj + k) >> 2;
-      if (need + 1 >= j0 + 9) {  // refill (chunks over ~28 bytes)
-        j0 = need;
-#pragma unroll
-        for (uint32_t i = 0; i < 9; i++) vj[i] = (j0 + i < nsrc[j]) ? sj[j0 + i] : 0u;
-      }
-      uint32_t w = word_at(k, vj, j0);
-      const uint32_t rem = szj - k;
-      if (rem >= 4) {
-        *reinterpret_cast<uint32_t*>(out + P + k) = w;
-      } else if (has_next && P + k + 4 <= cap) {  // complete the dword with the next chunk's first bytes
-        w = (w & ((1u << (8 * rem)) - 1u)) | (nh << (8 * rem));
-        *reinterpret_cast<uint32_t*>(out + P + k) = w;
-      } else {  // the plane's last chunk (the next plane's header follows), or the end of `cap`
-        for (uint32_t i = 0; i < rem; i++) out[P + k + i] = (uint8_t)(w >> (8 * i));
-      }
+    uint32_t w = word_at(k, v, j0);
+    const uint32_t rem = sz - k;
+    if (rem >= 4) {
+      *reinterpret_cast<uint32_t*>(out + P + k) = w;
+    } else if (has_next && P + k + 4 <= cap) {  // complete the dword with the next chunk's first bytes
+      w = (w & ((1u << (8 * rem)) - 1u)) | (nh << (8 * rem));
+      *reinterpret_cast<uint32_t*>(out + P + k) = w;
+    } else {  // the plane's last chunk (the next plane's header follows), or the end of `cap`
+      for (uint32_t i = 0; i < rem; i++) out[P + k + i] = (uint8_t)(w >> (8 * i));
     }
   }
 }

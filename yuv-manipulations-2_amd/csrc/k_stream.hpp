@@ -10,13 +10,6 @@ namespace myyuv_gpu {
 constexpr uint32_t kScanPerThread = MYYUV_SCAN_PER_THREAD;
 constexpr uint32_t kScanTile = 256 * kScanPerThread;
 
-// Tiles per workgroup of the stream writer k_stream_out (their loads in
-// flight together; k_stream.hip)
-#ifndef MYYUV_K4_TILES
-#define MYYUV_K4_TILES 1
-#endif
-constexpr uint32_t kK4Tiles = MYYUV_K4_TILES;
-
 // Where the u8 chunk-size bytes of each plane live in `src`.
 struct ScanSrc {
   uint32_t cum[4];  // plane block boundaries (global block numbering)

@@ -440,7 +440,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   }
   e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(256), s, c->tinfo.as<uint32_t>(), G,
               static_cast<uint8_t*>(d_out), cap, d_size, err);
-  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(ceil_div(G.tcum[3], kK4Tiles), nf), dim3(256), s,
+  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
               c->stage.as<const uint32_t>(), c->tinfo.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
               c->srcoff.as<const uint32_t>(), c->oslots.as<const uint32_t>(), G, static_cast<uint8_t*>(d_out),
               cap);

@@ -100,8 +100,22 @@ __device__ __forceinline__ uint32_t unit_stride() { return gridDim.x * 4u; }
 // kSkip: a step k whose P[2k], P[2k+1] are zero in every lane of the wave is
 // skipped (the sums start at +0 and a +-0 product leaves a sum unchanged, so
 // the result is bit-identical; see K6).
-template <bool kInverse, bool kSkip = false>
+template <bool kInverse, bool kSkip = false, bool kFma = false>
 __device__ __forceinline__ void dot_rows(const float (&P)[16], float (&out)[16]) {
+  static_assert(!(kSkip && kFma), "the FMA form is the forward fast path only");
+  if (kFma) {  // the fast path's chain: one rounding per term (bounded against the reference, fdct_core)
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+#pragma unroll
+      for (int v = 0; v < 8; v++) {
+        const float d = c_dct[kInverse ? k * 8 + v : v * 8 + k];
+        out[2 * v] = k == 0 ? P[0] * d : __builtin_fmaf(P[2 * k], d, out[2 * v]);
+        out[2 * v + 1] = k == 0 ? P[1] * d : __builtin_fmaf(P[2 * k + 1], d, out[2 * v + 1]);
+      }
+      fence16(out);
+    }
+    return;
+  }
   if (kSkip) {
 #pragma unroll
     for (int j = 0; j < 16; j++) out[j] = 0.0f;
@@ -188,12 +202,61 @@ __device__ __forceinline__ void load_quads(const uint4* __restrict__ coef, const
 }
 
 
+// Stage 1 of the forward transform for lane (b, q): T[2i + c] = T[i][2q + c] =
+// sum_k D[i][k] * X[k][2q + c] (squareMatrixMul<8>(DCT, X), DCT.cpp:232-242)
+// from the lane's pixel columns xr (signed bytes, row pairs): the reference's
+// order and roundings (kFma false), or an FMA chain (the fast path).
+template <bool kFma>
+__device__ __forceinline__ void fdct_stage1(const uint32_t (&xr)[4], float (&T)[16]) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float x0 = sbyte(xr[k >> 1], 2 * (k & 1)), x1 = sbyte(xr[k >> 1], 2 * (k & 1) + 1);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const float d = c_dct[i * 8 + k];
+      if (kFma) {
+        T[2 * i] = k == 0 ? d * x0 : __builtin_fmaf(d, x0, T[2 * i]);
+        T[2 * i + 1] = k == 0 ? d * x1 : __builtin_fmaf(d, x1, T[2 * i + 1]);
+      } else {
+        const float p0 = d * x0, p1 = d * x1;
+        T[2 * i] = k == 0 ? p0 : T[2 * i] + p0;
+        T[2 * i + 1] = k == 0 ? p1 : T[2 * i + 1] + p1;
+      }
+    }
+    fence16(T);
+  }
+}
+
+// Bound of |Y_fast - Y_ref| for the fast forward path (FMA chains in both
+// stages) against the reference's products and sums (recursive dot products,
+// Higham's gamma_8 bound per stage, |D| <= 0.5):
+//   |T_fast[i][k] - T_ref[i][k]| <= 2 g8 dmax A_k   (A_k = sum_m |X[m][k]|)
+//   |Y_fast[i][v] - Y_ref[i][v]| <= 2 g8 dmax (S_i + dmax A) (1 + g8)
+// with S_i = sum_k |T_fast[i][k]| and A = sum |X| over the block; kFastBound
+// = 2 g8 dmax (1 + 2^-10) (g8 = 8u / (1 - 8u), u = 2^-24; 4.7730e-7), rounded
+// up, which also covers the float evaluation of S_i and of the bound itself.
+constexpr float kFastBound = 4.79e-7f;
+
 // Forward transform + quantisation of lane (b, q)'s part of one block of a
 // 16-block unit (K1's per-unit body, DCT.cpp:269-277, :297-306): the block's
 // 8 pixel rows are in img (8 x 8 B, aliasing its transpose tile tb); out:
 // c[2v + h] holds, in its low 16 bits, the int16 coefficient of row 2q + h,
 // column v.  sqr: the Q tables then their reciprocals (QTables layout), p the
 // plane.
+//
+// Fast path (round 4): both stages as FMA chains (8 instructions per output
+// and stage instead of 15), then t = Y * fl(1/Q) rounded with the magic add.
+// Exactness: the reference's coefficient is roundf(fl(Y_ref / Q)).  With
+// |Y_fast - Y_ref| <= B (kFastBound, per row) and |fl(Y_ref / Q) - t| <=
+// B * r * (1 + 2^-20) + |t| * 2^-21 =: beta (the divide's and the
+// reciprocal's roundings in the second term), every output whose t lies
+// further than beta from the nearest half-integer rounds to the reference's
+// integer: fl(Y_ref / Q) is then strictly inside the same (n - 1/2, n + 1/2).
+// If any output of the wave's unit is closer, the wave recomputes the unit in
+// the reference's order and quantises as before (the near-tie lanes with the
+// reference's divide).  On the bench frame (4032x3008, q=50) 12 of 17,766
+// units take the exact path (0.07 %; 12.6 % of the units need the near-tie
+// divide at q=90 today, 18 % the exact path; tools/diag/fast_dct_sim.py).
 __device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_t q, const float* sqr, int p,
                                           uint32_t (&c)[16]) {
   const uint32_t n0 = 16u * q;
@@ -206,44 +269,63 @@ __device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_
              ((uint32_t)*reinterpret_cast<const uint16_t*>(img + 16 * m + 8 + 2 * q) << 16)) ^
             0x80808080u;
   wave_sync();
-  // ---- stage 1: T[i][j] = sum_k D[i][k] * X[k][j], j in {2q, 2q+1}
-  // (squareMatrixMul<8>(DCT, X), DCT.cpp:232-242); T[2i + c] = T[i][2q + c]
+  // ---- A = sum |x| over the block (exact: byte SADs against 128, the
+  // block's four lanes summed)
+  uint32_t a = 0;
+#pragma unroll
+  for (int m = 0; m < 4; m++) a = __builtin_amdgcn_sad_u8(xr[m] ^ 0x80808080u, 0x80808080u, a);
+  a += (uint32_t)__shfl_xor((int)a, 1, 64);
+  a += (uint32_t)__shfl_xor((int)a, 2, 64);
+  // ---- stage 1 (fast), transpose: columns (2q, 2q+1) in, rows (2q, 2q+1) out
   float T[16];
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const float x0 = sbyte(xr[k >> 1], 2 * (k & 1)), x1 = sbyte(xr[k >> 1], 2 * (k & 1) + 1);
-    float pr[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      pr[2 * i] = c_dct[i * 8 + k] * x0;
-      pr[2 * i + 1] = c_dct[i * 8 + k] * x1;
-    }
-#pragma unroll
-    for (int j = 0; j < 16; j++) T[j] = k == 0 ? pr[j] : T[j] + pr[j];
-    fence16(T);
-  }
-  // ---- transpose: columns (2q, 2q+1) in, rows (2q, 2q+1) out
+  fdct_stage1<true>(xr, T);
   float P[16];  // P[2k + h] = T[2q + h][k]
   transpose_tile(tb, q, T, P);
-  // ---- stage 2: Y[i][v] = sum_k T[i][k] * D[v][k] (squareMatrixMulT<8>(T, DCT),
+  float s0 = 0.0f, s1 = 0.0f;  // S_h = sum_k |T[2q + h][k]|
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    s0 += __builtin_fabsf(P[2 * k]);
+    s1 += __builtin_fabsf(P[2 * k + 1]);
+  }
+  // ---- stage 2 (fast): Y[i][v] = sum_k T[i][k] * D[v][k] (squareMatrixMulT<8>(T, DCT),
   // DCT.cpp:244-254); coef = (int16)roundf(Y / Q) (DCT.cpp:273-276)
   float Y[16];  // Y[2v + h] = Y[2q + h][v]
-  dot_rows<false>(P, Y);
+  dot_rows<false, false, true>(P, Y);
+  const float af = 0.5f * (float)a;
+  const float b0 = kFastBound * (s0 + af) * (1.0f + 0x1p-20f), b1 = kFastBound * (s1 + af) * (1.0f + 0x1p-20f);
   // reciprocals of rows 2q, 2q+1 (natural n0 .. n0 + 15)
   const float4* R4 = reinterpret_cast<const float4*>(sqr + 3 * 64 + p * 64 + n0);
   const float4 r0 = R4[0], r1 = R4[1], r2 = R4[2], r3 = R4[3];
   const float rr[16] = {r0.x, r2.x, r0.y, r2.y, r0.z, r2.z, r0.w, r2.w,
                         r1.x, r3.x, r1.y, r3.y, r1.z, r3.z, r1.w, r3.w};  // [2v + h]
-  float mx = 0.0f;  // max over the lane of |e| + |t| * 2^-21: >= 0.5 near a tie
+  float mx = 0.0f;  // max over the lane of |e| + beta: >= 0.5 when an output may round otherwise
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const float tq = Y[j] * rr[j];
+    const float e = tq - ((tq + kMagic) - kMagic);
+    mx = __builtin_fmaxf(mx, __builtin_fmaf((j & 1) ? b1 : b0, rr[j],
+                                            __builtin_fmaf(__builtin_fabsf(tq), kNearRel, __builtin_fabsf(e))));
+  }
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(mx >= 0.5f) != 0, 0)) {
+    // ---- the unit in the reference's order (wave-uniform branch): Y is
+    // replaced by the reference's values, quantised below as before
+    wave_sync();  // (the tile is rewritten)
+    fdct_stage1<false>(xr, T);
+    transpose_tile(tb, q, T, P);
+    dot_rows<false>(P, Y);
+  }
+  // ---- quantisation (fast Y: every output clears the bound above, so the
+  // near-tie test below never fires for it; reference Y: as before)
+  float mx2 = 0.0f;  // max over the lane of |e| + |t| * 2^-21: >= 0.5 near a tie
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     const float tq = Y[j] * rr[j];
     const float uu = tq + kMagic;
     const float e = tq - (uu - kMagic);
-    mx = __builtin_fmaxf(mx, __builtin_fmaf(__builtin_fabsf(tq), kNearRel, __builtin_fabsf(e)));
+    mx2 = __builtin_fmaxf(mx2, __builtin_fmaf(__builtin_fabsf(tq), kNearRel, __builtin_fabsf(e)));
     c[j] = bits(uu);
   }
-  if (mx >= 0.5f) {  // a near-tie in the lane: the reference's divide for all 16
+  if (mx2 >= 0.5f) {  // a near-tie in the lane: the reference's divide for all 16
     const float* Qt = sqr + p * 64 + n0;
 #pragma unroll
     for (int j = 0; j < 16; j++) c[j] = (uint32_t)(int)roundf(Y[j] / Qt[(j >> 1) + 8 * (j & 1)]);
