@@ -48,14 +48,16 @@ order at N = 1).
 
 roofline: K1 fdct_quant, the block-transform kernel of the north star.
 Algorithmic bytes = 3 B per sample (1 B u8 in + 2 B int16 out)
-x the samples of the launches; time = those launches' HIP-event durations
+x the samples of the launches; time = those launches' HIP-event durations,
+K1's own plus those of k_fdct_fix (K1's exact path for the units whose fast
+result it cannot prove; it runs right after K1 in the stream)
 (dispatch-stamped on their streams, every launch group's K1 by default,
 --events-ctx0: group 0's only) over the timed region, where K1 shares the GPU
 with the other groups in flight.  `traffic` = calibrated FETCH_SIZE/WRITE_SIZE
 bytes per launch from the newest rocprofv3 --pmc profile of this workload
 under profiles/ (null if none); `traffic_gbs` = traffic / avg launch time.
 K1 is VALU-issue bound: `valu_ceiling_frac` is the fraction of
-the HBM peak its bit-exact arithmetic alone allows (the gfx950 code object's
+the HBM peak its fast path's instructions alone allow (the gfx950 code object's
 VALU count per 16-block unit at the 2-cycle f32 issue rate on 1,024 SIMDs at
 the effective clock), so `frac` reads against it.  roofline_isolated: the
 same K1 figure from the untimed one-group-at-a-time breakdown pass.
@@ -107,13 +109,13 @@ BIG_DECODED_SHA = "5e7769191188285cc127c6b4da900b3420f064191f707383c82128c14e497
 BIG_RECOMPRESSED_SHA = "fe9b7317653c2b44a9f24436f0e349b083b4e368cf9653e8777e9f7a79cebfcc"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8 TB/s spec)
 SLOT_4K = 4 << 20  # batch4k payload slot: the largest of the 512 streams is 2,471,404 B (capacity is checked on device)
-# K1's bit-exact VALU work (tools/kdis.sh on the gfx950 code
-# object): VALU instructions per lane per 16-block unit, of which the
-# reference's own fp32 products and sums; f32 VALU issue = 2 cycles per
+# K1's VALU work (the gfx950 code object's loop body): VALU
+# instructions per lane per 16-block unit on the fast path, of which the
+# transform's FMA chains (round 3's reference-order path: 660, 480); f32 VALU issue = 2 cycles per
 # wave-instruction (64 lanes on a 32-wide SIMD), 1,024 SIMDs, effective clock
 # under load from GRBM_GUI_ACTIVE (profiles/r02b_sq_counters.txt)
-K1_VALU_PER_UNIT = 660
-K1_ARITH_PER_UNIT = 480
+K1_VALU_PER_UNIT = 488
+K1_ARITH_PER_UNIT = 256
 K1_CLOCK_GHZ = 1.7
 
 
@@ -748,16 +750,19 @@ def k1_roofline(stats, samples_per_frame, frames, B, frame_key):
     k1_ms, k1_n = stats.get("fdct_quant", (0.0, 0))
     if not k1_n or not frames:
         return None
+    fix_ms, fix_n = stats.get("fdct_fix", (0.0, 0))
+    k1_ms += fix_ms
     alg_total = 3 * samples_per_frame * frames
     achieved = alg_total / (k1_ms / 1e3) / 1e9
     avg_s = k1_ms / k1_n / 1e3
     traffic = load_traffic(frame_key, B)
     ceil = valu_ceiling_frac(samples_per_frame)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "fdct_quant",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "fdct_quant+fdct_fix",
+            "fix_avg_us": round(fix_ms / fix_n * 1e3, 2) if fix_n else None,
             "algorithmic_bytes_per_launch": alg_total // k1_n, "avg_launch_us": round(avg_s * 1e6, 2),
             "valu_ceiling_frac": ceil,
-            "issue_bound": "valu (bit-exact reference-order fp32 sums, DESIGN.md §4)"}
+            "issue_bound": "valu (fp32 FMA chains checked against a rigorous error bound, DESIGN.md §4)"}
     if traffic:
         roof["traffic_gbs"] = round(traffic / avg_s / 1e9, 1)
         roof["traffic_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
@@ -862,7 +867,7 @@ def main(argv=None):
     if gpu and not args.no_kernel_events:
         stamped = codec.codecs[:1] if args.events_ctx0 else codec.codecs
         for c in stamped:
-            c.profile(True, kernels=["fdct_quant"])
+            c.profile(True, kernels=["fdct_quant", "fdct_fix"])
     t, got = run.timed(args.steps, dist, dev, args.gather_chunk)
     checked(codec.check, "the timed region", dist, world, rank, dev, bad_ranks=run.gather_bad)
     stats = {}
@@ -911,9 +916,10 @@ def main(argv=None):
         # breakdown pass): the kernel alone on the GPU, no co-running group
         roof_iso = None
         if roof and kernel_us.get("fdct_quant"):
-            a_iso = 3 * run.samples * run.B / (kernel_us["fdct_quant"] * 1e-6) / 1e9
+            k1_us = kernel_us["fdct_quant"] + kernel_us.get("fdct_fix", 0.0)
+            a_iso = 3 * run.samples * run.B / (k1_us * 1e-6) / 1e9
             roof_iso = {"achieved": round(a_iso, 1), "frac": round(a_iso / HBM_PEAK_GBS, 4),
-                        "avg_launch_us": kernel_us["fdct_quant"]}
+                        "avg_launch_us": round(k1_us, 2)}
         # the fused decoder (default; K5 + K6 in one kernel, the "huff_decode"
         # id): stream bytes in + 1 B per sample out
         roof_dec = None

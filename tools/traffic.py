@@ -8,8 +8,8 @@ HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
 coalesced stream, so read bytes = 2 * FETCH_SIZE * 1024 for kernels whose
 reads are 16-B-per-lane streams, write bytes = WRITE_SIZE * 1024.  K1's 8-B
-row loads / 16-B quad stores and K6's quad loads / 8-B row stores have their
-own factors, measured on known byte counts with the same addressing
+row loads / 16-B quad stores, K6's quad loads / 8-B row stores, K2's
+scattered row loads and K4's gathers have their own factors, measured on known byte counts with the same addressing
 (tools/ubench/calib.hip -> profiles/<tag>_calib.json, newest one used).
 """
 import collections
@@ -30,8 +30,15 @@ def per_kernel(path):
     return {k: sum(v) / len(v) for k, v in d.items()}
 
 
-# codec kernel -> (read shape, write shape) of tools/ubench/calib.hip
-CALIB_SHAPES = {"fdct_quant": ("k1_read", "k1_write"), "dequant_idct": ("k6_read", "k6_write")}
+# codec kernel -> (read shape, write shape) of tools/ubench/calib.hip.  K2's
+# reads are dominated by its scattered per-lane 16-B row loads (runs of
+# blocks), whose FETCH_SIZE counts the bytes once (factor ~1, not 2,
+# profiles/r4b_calib.json); its classify pass's coalesced rmask/DC reads
+# (factor 2) are ~5 % of the bytes, so the K2 figures are a lower bound
+# within that.  K4 gathers 16-B words coalesced (factor 2).
+CALIB_SHAPES = {"fdct_quant": ("k1_read", "k1_write"), "dequant_idct": ("k6_read", "k6_write"),
+                "huff_encode": ("k2_scatter_read", None), "huff_encode_r16": ("k2_scatter_read", None),
+                "huff_encode_wide": ("k2_scatter_read", None), "stream_out": ("k4_gather_read", None)}
 
 
 def calib_factors():
@@ -58,8 +65,9 @@ def main(tag):
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"))
     cf, cname = calib_factors()
     out = {"_note": "bytes per launch; read = 2 x FETCH_SIZE (gfx950 wide-stream correction), "
-                    "write = WRITE_SIZE; both KiB x 1024; fdct_quant / dequant_idct use the factors "
-                    f"measured for their own access shapes ({cname}); avg_ns from the kernel-trace pass"}
+                    "write = WRITE_SIZE; both KiB x 1024; fdct_quant / dequant_idct / huff_encode* / "
+                    f"stream_out use the factors measured for their own access shapes ({cname}: "
+                    "K2's scattered row loads count once, factor ~1); avg_ns from the kernel-trace pass"}
     for k in sorted(set(fetch) | set(write)):
         if k.startswith("__amd") or "at::native" in k:
             continue

@@ -1348,16 +1348,16 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
     *reinterpret_cast<uint2*>(img + 16u * q) = make_uint2(rows.px[i].x, rows.px[i].y);
     *reinterpret_cast<uint2*>(img + 16u * q + 8u) = make_uint2(rows.px[i].z, rows.px[i].w);
     wave_sync();
-    uint32_t c[16];
-    fdct_core(img, tb, q, s_q, p, c);
-    uint4 lo, hi;
-    uint32_t rm;
-    pack_quads(c, q, lo, hi, rm);
-    if (lb < nloc) {
-      s_img[(2 * q) * kK2Group + lb] = lo;
-      s_img[(2 * q + 1) * kK2Group + lb] = hi;
-      if (q == 0) s_rmk[lb] = (uint8_t)rm;
-    }
+    fdct_core(img, tb, q, s_q, p, [&](const uint32_t (&c)[16]) {
+      uint4 lo, hi;
+      uint32_t rm;
+      pack_quads(c, q, lo, hi, rm);
+      if (lb < nloc) {
+        s_img[(2 * q) * kK2Group + lb] = lo;
+        s_img[(2 * q + 1) * kK2Group + lb] = hi;
+        if (q == 0) s_rmk[lb] = (uint8_t)rm;
+      }
+    });
     wave_sync();  // the tile is rewritten by the next unit
   }
   __syncthreads();

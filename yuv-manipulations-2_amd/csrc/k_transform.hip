@@ -86,10 +86,46 @@ using namespace xf;
 
 // K1: u8 planes -> int16 coefficients (natural order, quad layout).
 // DCT.cpp:297-306 (gather, x - 128), :269-277 (applyDCTBlock).
+// Rows 2q, 2q+1 of lane (b, q)'s block (coefficient quads 2q, 2q+1) and the
+// block's row mask for K2 (bit c: row c has a nonzero coefficient, from the
+// block's four lanes).  An all-zero row is not stored (K2 reads masked-off
+// rows from a zero buffer), which saves most of the 128 B per block of a
+// q=50 frame twice (this write, K2's read).  Every lane still issues its three
+// stores (the sink takes the skipped ones and those of lanes past the
+// plane's end).
+__device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32_t q, uint32_t lane, bool live,
+                                                 uint32_t g, uint4* dlo, uint4* dhi, uint8_t* __restrict__ rmask,
+                                                 uint4* __restrict__ sink) {
+  uint4 lo, hi;
+  uint32_t rm;
+  pack_quads(c, q, lo, hi, rm);
+#if MYYUV_EXP == 2
+  if ((lo.x ^ hi.y ^ lo.z ^ hi.w ^ rm) == 0x7f3e5a11u) {  // never (keeps the transform live)
+    *dlo = lo;
+    *dhi = hi;
+  }
+#else
+  const bool nzl = (rm >> (2 * q)) & 1u, nzh = (rm >> (2 * q + 1)) & 1u;
+  *(live ? rmask + g : reinterpret_cast<uint8_t*>(sink + 128) + lane) = (uint8_t)rm;
+  *(nzl ? dlo : sink + lane) = lo;
+  *(nzh ? dhi : sink + 64 + lane) = hi;
+#endif
+}
+
+// K1's exact path out of line (MYYUV_K1_INLINE_EXACT 0): a unit whose fast
+// result is not provably the reference's is listed in fix (fix[par] the
+// count, fix[64 + i] the batch unit; par alternates from launch to launch) by
+// K1 and transformed by k_fdct_fix, which runs next in the stream.  Kept in K1, the exact path's code raised K1 from 64 to
+// 99 VGPRs (7 -> 5 waves per SIMD) and cost it 15 % (profiles/r4g_*).
+#ifndef MYYUV_K1_INLINE_EXACT
+#define MYYUV_K1_INLINE_EXACT 0
+#endif
+
 __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t* __restrict__ frame, FrameGeom G,
                                                    const QTables* __restrict__ qt,
                                                    uint4* __restrict__ coef, uint8_t* __restrict__ rmask,
-                                                   uint4* __restrict__ sink, uint32_t* __restrict__ k2ctl) {
+                                                   uint4* __restrict__ sink, uint32_t* __restrict__ k2ctl,
+                                                   uint32_t* __restrict__ fix, uint32_t par) {
 #if MYYUV_K1_PRIO > 0
   // wave issue priority over the other launch groups' kernels on the SIMD
   __builtin_amdgcn_s_setprio(MYYUV_K1_PRIO);
@@ -150,31 +186,53 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
     }
     continue;
 #endif
-    uint32_t c[16];
-    fdct_core(img, tb, q, sqr, U.p, c);
-
-    // ---- store rows 2q, 2q+1 = coefficient quads 2q, 2q+1 of the block
-    {
-      uint4 lo, hi;
-      uint32_t rm;
-      pack_quads(c, q, lo, hi, rm);
-#if MYYUV_EXP == 2
-      if ((lo.x ^ hi.y ^ lo.z ^ hi.w ^ rm) == 0x7f3e5a11u) {  // never (keeps the transform live)
-        *dlo = lo;
-        *dhi = hi;
-      }
+    auto store = [&](const uint32_t (&c)[16]) { store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, sink); };
+#if MYYUV_K1_INLINE_EXACT
+    fdct_core(img, tb, q, sqr, U.p, store);
 #else
-      // Row mask for K2 (bit c: row c has a nonzero coefficient), from the
-      // block's four lanes; an all-zero row is not stored (K2 reads masked-off
-      // rows from a zero buffer), which saves most of the 128 B per block of
-      // a q=50 frame twice (this write, K2's read).  Every lane still issues
-      // its three stores (the sink takes the skipped ones).
-      const bool nzl = (rm >> (2 * q)) & 1u, nzh = (rm >> (2 * q + 1)) & 1u;
-      *(live ? rmask + g : reinterpret_cast<uint8_t*>(sink + 128) + lane) = (uint8_t)rm;
-      *(nzl ? dlo : sink + lane) = lo;
-      *(nzh ? dhi : sink + 64 + lane) = hi;
+    uint32_t xr[4];
+    fdct_load(img, q, xr);
+    if (!fdct_fast(xr, tb, q, sqr, U.p, store) && lane == 0) fix[64 + atomicAdd(fix + par, 1u)] = ua;
 #endif
-    }
+  }
+}
+
+// K1's exact path for the units K1 listed (fix[par] of them at fix + 64): a
+// wave per listed unit, the reference's order (fdct_exact), the same stores.
+// Workgroup 0 zeroes the other parity's count, which the next K1 fills (the
+// previous fix launch, its reader, is done: stream order).
+__global__ __launch_bounds__(256) void k_fdct_fix(const uint8_t* __restrict__ frame, FrameGeom G,
+                                                  const QTables* __restrict__ qt, uint4* __restrict__ coef,
+                                                  uint8_t* __restrict__ rmask, uint4* __restrict__ sink,
+                                                  uint32_t* __restrict__ fix, uint32_t par) {
+  __shared__ float tile[4][kXfUnit * kTile];
+  __shared__ float sqr[2 * 3 * 64];
+  if (blockIdx.x == 0 && threadIdx.x == 0) fix[par ^ 1u] = 0u;
+  const uint32_t n = __builtin_amdgcn_readfirstlane(fix[par]);
+  if (blockIdx.x * 4u >= n) return;  // (uniform over the workgroup)
+  stage_tables<2 * 3 * 64>(qt->q[0], sqr);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t q = lane & 3u, b = lane >> 2;
+  float* tb = tile[threadIdx.x >> 6] + b * kTile;
+  uint8_t* img = reinterpret_cast<uint8_t*>(tb);
+  for (uint32_t i = first_unit(); i < n; i += unit_stride()) {
+    const uint32_t ua = __builtin_amdgcn_readfirstlane(fix[64 + i]);
+    const uint32_t f = div_magic(ua, G.umag);
+    const Unit U = unit_of(G, ua - f * G.ucum[3]);
+    const uint32_t local = U.local0 + b;
+    const bool live = local < U.nb;
+    const uint32_t g = f * G.cum[3] + U.cum + local;
+    const uint4 r = load_rows(frame, G, ua, b, q);
+    wave_sync();  // (the previous unit's tile reads are done)
+    *reinterpret_cast<uint2*>(img + 16u * q) = make_uint2(r.x, r.y);
+    *reinterpret_cast<uint2*>(img + 16u * q + 8u) = make_uint2(r.z, r.w);
+    wave_sync();
+    uint4* dlo = live ? coef + coef_quad(g, 2 * q) : sink + lane;
+    uint4* dhi = live ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
+    uint32_t xr[4];
+    fdct_load(img, q, xr);
+    fdct_exact(xr, tb, q, sqr, U.p,
+               [&](const uint32_t (&c)[16]) { store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, sink); });
   }
 }
 

@@ -27,7 +27,10 @@
 #endif
 
 namespace myyuv_gpu {
-__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*);
+__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*,
+                             uint32_t*, uint32_t);
+__global__ void k_fdct_fix(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*,
+                           uint32_t);
 __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*,
                                uint4*);
 __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*, const uint32_t*,
@@ -187,7 +190,14 @@ struct myyuv_hip_ctx {
   DevBuf rmask; // per block: bit c = coefficient row c nonzero (K5 -> K6)
   DevBuf zq;    // 256 zero bytes: K6's source for rows the mask says are zero
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
+  // K1 -> k_fdct_fix: [0], [1] the unit counts of even / odd launches
+  // (fix_par), from [64] the units
+  DevBuf fix;
+  uint32_t fix_par = 0;
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
+  uint32_t fix_resident = kXfWaves / 4;                      // k_fdct_fix workgroups resident
+  uint32_t fix_grid = 64;  // k_fdct_fix's grid at qualities up to fix_qmax (MYYUV_FIX_GRID, 0: resident)
+  uint32_t fix_qmax = 75;  // (MYYUV_FIX_QMAX)
   // encoder: K1 -> K2 through HBM (split), or the fused single-pass kernel
   // k_encode_tile (MYYUV_ENCODER=fused|split)
   bool fused = false;
@@ -337,6 +347,14 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
   // [0], [1]: overflow counts, then K2's list and (single frames) the CAP-16 tier's (launch_overflow)
   e |= c->work.grow((size_t)nblk * (nf == 1 || MYYUV_R16_BATCH ? 8 : 4) + 256);
+  {
+    const size_t fb = ((size_t)G.ucum[3] * nf + 64) * 4;
+    if (c->fix.n < fb) {
+      e |= c->fix.grow(fb);
+      if (!e && (hipMemset(c->fix.p, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+        e |= MYYUV_E_HIP;
+    }
+  }
   const size_t st_bytes = (size_t)nf * (ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
@@ -413,6 +431,30 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   return e;
 }
 
+// K1, then its exact path for the units it listed (k_fdct_fix).  The list
+// is on the device, so the fix grid cannot follow its length: fix_grid
+// workgroups (4 waves each) where the quality keeps it short, the resident
+// count otherwise (the fast path fails for 0.07 % of the bench frame's units
+// at q50, 18 % at q90, 48 % at q100: tools/diag/fast_dct_sim.py); workgroups
+// past the list return at once.  k2ctl: K2's overflow count, zeroed by K1
+// (nullptr: none).
+int launch_fdct(myyuv_hip_ctx* c, const FrameGeom& G, const uint8_t* in, const QTables* qt, uint32_t* k2ctl,
+                hipStream_t s) {
+  const uint32_t par = c->fix_par;
+  c->fix_par ^= 1u;
+  int e = launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s, in, G, qt,
+                 c->coef.as<uint4>(), c->rmask.as<uint8_t>(), c->sink.as<uint4>(), k2ctl, c->fix.as<uint32_t>(),
+                 par);
+  uint32_t qmax = 0;
+  for (int p = 0; p < 3; p++) qmax = std::max(qmax, (uint32_t)c->q_cached[p]);
+  const uint32_t want =
+      (c->fix_grid == 0 || !c->q_valid || qmax > c->fix_qmax) ? c->fix_resident : c->fix_grid;
+  const uint32_t grid = std::max(1u, std::min(want, ceil_div(G.ucum[3] * G.nframes, 4)));
+  e |= launch(c, MYYUV_K_FDCT_FIX, k_fdct_fix, dim3(grid), dim3(256), s, in, G, qt, c->coef.as<uint4>(),
+              c->rmask.as<uint8_t>(), c->sink.as<uint4>(), c->fix.as<uint32_t>(), par);
+  return e;
+}
+
 // One batch of G.nframes frames (frame f at d_in + f * fbytes), payload f at
 // d_out + f * cap, its size at d_size[f].
 int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void* d_out,
@@ -431,9 +473,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
                 count + 64, count);
     e |= launch_overflow(c, G, s);
   } else {
-    e |= launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s,
-                static_cast<const uint8_t*>(d_in), G, qt, c->coef.as<uint4>(), c->rmask.as<uint8_t>(),
-                c->sink.as<uint4>(), c->work.as<uint32_t>());
+    e |= launch_fdct(c, G, static_cast<const uint8_t*>(d_in), qt, c->work.as<uint32_t>(), s);
     if ((c->skip >> MYYUV_K_FDCT) & 1u)  // diagnostic skip: keep K1's reset of the overflow count
       e |= hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess;
     e |= launch_huff_encode(c, G, s);
@@ -607,6 +647,11 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
         cus > 0 && n1 > 0 && n6 > 0) {
       c->xf_resident[0] = (uint32_t)(cus * n1);
       c->xf_resident[1] = (uint32_t)(cus * n6);
+      int nfix = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nfix, k_fdct_fix, 256, 0) == hipSuccess && nfix > 0)
+        c->fix_resident = (uint32_t)(cus * nfix);
+      if (const char* v = std::getenv("MYYUV_FIX_GRID")) c->fix_grid = (uint32_t)std::atoi(v);
+      if (const char* v = std::getenv("MYYUV_FIX_QMAX")) c->fix_qmax = (uint32_t)std::atoi(v);
       {
         const char* v = std::getenv("MYYUV_ENCODER");
         c->fused = v && std::strcmp(v, "fused") == 0;
@@ -1055,9 +1100,8 @@ int myyuv_gpu_fdct_blocks(myyuv_hip_handle c, const uint8_t* px, uint32_t nblock
       hipMemcpy(c->qtd.p, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->frame.p, px, (size_t)nblocks * 64, hipMemcpyHostToDevice) != hipSuccess)
     return MYYUV_E_HIP;
-  hipLaunchKernelGGL(k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), 0, s,
-                     c->frame.as<const uint8_t>(), G, c->qtd.as<const QTables>(), c->coef.as<uint4>(),
-                     c->rmask.as<uint8_t>(), c->sink.as<uint4>(), (uint32_t*)nullptr);
+  if (launch_fdct(c, G, c->frame.as<const uint8_t>(), c->qtd.as<const QTables>(), nullptr, s))
+    return MYYUV_E_HIP;
   std::vector<uint32_t> words((size_t)ceil_div(nblocks, kWave) * kCoefQuadsPerWave * 4);
   std::vector<uint8_t> rm(nblocks);
   if (hipGetLastError() != hipSuccess ||

@@ -238,11 +238,12 @@ __device__ __forceinline__ void fdct_stage1(const uint32_t (&xr)[4], float (&T)[
 constexpr float kFastBound = 4.79e-7f;
 
 // Forward transform + quantisation of lane (b, q)'s part of one block of a
-// 16-block unit (K1's per-unit body, DCT.cpp:269-277, :297-306): the block's
-// 8 pixel rows are in img (8 x 8 B, aliasing its transpose tile tb); out:
-// c[2v + h] holds, in its low 16 bits, the int16 coefficient of row 2q + h,
-// column v.  sqr: the Q tables then their reciprocals (QTables layout), p the
-// plane.
+// 16-block unit (K1's per-unit body, DCT.cpp:269-277, :297-306), in three
+// pieces: fdct_load (the lane's pixel columns from the block's 8 x 8 B image
+// img, which aliases its transpose tile tb), fdct_fast and fdct_exact.  The
+// lane's 16 coefficients go to emit(c): c[2v + h] holds, in its low 16 bits,
+// the int16 coefficient of row 2q + h, column v.  sqr: the Q tables then
+// their reciprocals (QTables layout), p the plane.
 //
 // Fast path (round 4): both stages as FMA chains (8 instructions per output
 // and stage instead of 15), then t = Y * fl(1/Q) rounded with the magic add.
@@ -252,23 +253,28 @@ constexpr float kFastBound = 4.79e-7f;
 // reciprocal's roundings in the second term), every output whose t lies
 // further than beta from the nearest half-integer rounds to the reference's
 // integer: fl(Y_ref / Q) is then strictly inside the same (n - 1/2, n + 1/2).
-// If any output of the wave's unit is closer, the wave recomputes the unit in
-// the reference's order and quantises as before (the near-tie lanes with the
+// If any output of the wave's unit is closer, fdct_fast emits nothing and
+// returns false (wave-uniform), and the unit goes through fdct_exact: the
+// reference's order, quantised as before (the near-tie lanes with the
 // reference's divide).  On the bench frame (4032x3008, q=50) 12 of 17,766
-// units take the exact path (0.07 %; 12.6 % of the units need the near-tie
-// divide at q=90 today, 18 % the exact path; tools/diag/fast_dct_sim.py).
-__device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_t q, const float* sqr, int p,
-                                          uint32_t (&c)[16]) {
-  const uint32_t n0 = 16u * q;
-  // ---- columns 2q, 2q+1 of the block's 8 rows; x ^ 0x80 is x - 128 as a
-  // signed byte (DCT.cpp:303)
-  uint32_t xr[4];  // rows 2m (low half), 2m+1 (high half)
+// units take the exact path (0.07 %; 18 % at q=90, 48 % at q=100;
+// tools/diag/fast_dct_sim.py).
+
+// The lane's columns 2q, 2q+1 of the block's 8 rows; x ^ 0x80 is x - 128 as
+// a signed byte (DCT.cpp:303).  xr[m]: rows 2m (low half), 2m+1 (high half).
+// The image may be overwritten after this (the wave_sync).
+__device__ __forceinline__ void fdct_load(const uint8_t* img, uint32_t q, uint32_t (&xr)[4]) {
 #pragma unroll
   for (int m = 0; m < 4; m++)
     xr[m] = (*reinterpret_cast<const uint16_t*>(img + 16 * m + 2 * q) |
              ((uint32_t)*reinterpret_cast<const uint16_t*>(img + 16 * m + 8 + 2 * q) << 16)) ^
             0x80808080u;
   wave_sync();
+}
+
+template <class Emit>
+__device__ __forceinline__ bool fdct_fast(const uint32_t (&xr)[4], float* tb, uint32_t q, const float* sqr, int p,
+                                          Emit&& emit) {
   // ---- A = sum |x| over the block (exact: byte SADs against 128, the
   // block's four lanes summed)
   uint32_t a = 0;
@@ -288,47 +294,83 @@ __device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_
     s1 += __builtin_fabsf(P[2 * k + 1]);
   }
   // ---- stage 2 (fast): Y[i][v] = sum_k T[i][k] * D[v][k] (squareMatrixMulT<8>(T, DCT),
-  // DCT.cpp:244-254); coef = (int16)roundf(Y / Q) (DCT.cpp:273-276)
-  float Y[16];  // Y[2v + h] = Y[2q + h][v]
-  dot_rows<false, false, true>(P, Y);
+  // DCT.cpp:244-254); coef = (int16)roundf(Y / Q) (DCT.cpp:273-276).  One
+  // column pair at a time, quantised as it is done (only P and two sums live;
+  // K1 292 against 334 us per 24-frame launch with all 16 sums in flight)
   const float af = 0.5f * (float)a;
   const float b0 = kFastBound * (s0 + af) * (1.0f + 0x1p-20f), b1 = kFastBound * (s1 + af) * (1.0f + 0x1p-20f);
+  // reciprocals of rows 2q, 2q+1 (natural 16q .. 16q + 15)
+  const float* Rq = sqr + 3 * 64 + p * 64 + 16u * q;
+  uint32_t c[16];
+  float mx = 0.0f;  // max over the lane of |e| + beta: >= 0.5 when an output may round otherwise
+#pragma unroll
+  for (int v = 0; v < 8; v++) {
+    float y0 = P[0] * c_dct[v * 8], y1 = P[1] * c_dct[v * 8];
+#pragma unroll
+    for (int k = 1; k < 8; k++) {
+      y0 = __builtin_fmaf(P[2 * k], c_dct[v * 8 + k], y0);
+      y1 = __builtin_fmaf(P[2 * k + 1], c_dct[v * 8 + k], y1);
+    }
+    const float r0 = Rq[v], r1 = Rq[8 + v];
+    const float t0 = y0 * r0, t1 = y1 * r1;
+    const float u0 = t0 + kMagic, u1 = t1 + kMagic;
+    const float e0 = t0 - (u0 - kMagic), e1 = t1 - (u1 - kMagic);
+    mx = __builtin_fmaxf(mx, __builtin_fmaf(b0, r0, __builtin_fmaf(__builtin_fabsf(t0), kNearRel, __builtin_fabsf(e0))));
+    mx = __builtin_fmaxf(mx, __builtin_fmaf(b1, r1, __builtin_fmaf(__builtin_fabsf(t1), kNearRel, __builtin_fabsf(e1))));
+    c[2 * v] = bits(u0);
+    c[2 * v + 1] = bits(u1);
+  }
+#ifndef MYYUV_FAST_ONLY  // (tuning builds only: no exact path, results may differ)
+  if (__builtin_amdgcn_ballot_w64(mx >= 0.5f) != 0) return false;
+#endif
+  emit(c);  // every output clears the bound: its rounded t is the reference's coefficient
+  return true;
+}
+
+// The unit in the reference's order (the tile tb is rewritten: callers
+// wave_sync between a fast attempt and this).
+template <class Emit>
+__device__ __forceinline__ void fdct_exact(const uint32_t (&xr)[4], float* tb, uint32_t q, const float* sqr, int p,
+                                           Emit&& emit) {
+  const uint32_t n0 = 16u * q;
+  float T[16];
+  fdct_stage1<false>(xr, T);
+  float P[16];  // P[2k + h] = T[2q + h][k]
+  transpose_tile(tb, q, T, P);
+  float Y[16];  // Y[2v + h] = Y[2q + h][v]
+  dot_rows<false>(P, Y);
   // reciprocals of rows 2q, 2q+1 (natural n0 .. n0 + 15)
   const float4* R4 = reinterpret_cast<const float4*>(sqr + 3 * 64 + p * 64 + n0);
   const float4 r0 = R4[0], r1 = R4[1], r2 = R4[2], r3 = R4[3];
   const float rr[16] = {r0.x, r2.x, r0.y, r2.y, r0.z, r2.z, r0.w, r2.w,
                         r1.x, r3.x, r1.y, r3.y, r1.z, r3.z, r1.w, r3.w};  // [2v + h]
-  float mx = 0.0f;  // max over the lane of |e| + beta: >= 0.5 when an output may round otherwise
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    const float tq = Y[j] * rr[j];
-    const float e = tq - ((tq + kMagic) - kMagic);
-    mx = __builtin_fmaxf(mx, __builtin_fmaf((j & 1) ? b1 : b0, rr[j],
-                                            __builtin_fmaf(__builtin_fabsf(tq), kNearRel, __builtin_fabsf(e))));
-  }
-  if (__builtin_expect(__builtin_amdgcn_ballot_w64(mx >= 0.5f) != 0, 0)) {
-    // ---- the unit in the reference's order (wave-uniform branch): Y is
-    // replaced by the reference's values, quantised below as before
-    wave_sync();  // (the tile is rewritten)
-    fdct_stage1<false>(xr, T);
-    transpose_tile(tb, q, T, P);
-    dot_rows<false>(P, Y);
-  }
-  // ---- quantisation (fast Y: every output clears the bound above, so the
-  // near-tie test below never fires for it; reference Y: as before)
-  float mx2 = 0.0f;  // max over the lane of |e| + |t| * 2^-21: >= 0.5 near a tie
+  uint32_t c[16];
+  float mx = 0.0f;  // max over the lane of |e| + |t| * 2^-21: >= 0.5 near a tie
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     const float tq = Y[j] * rr[j];
     const float uu = tq + kMagic;
     const float e = tq - (uu - kMagic);
-    mx2 = __builtin_fmaxf(mx2, __builtin_fmaf(__builtin_fabsf(tq), kNearRel, __builtin_fabsf(e)));
+    mx = __builtin_fmaxf(mx, __builtin_fmaf(__builtin_fabsf(tq), kNearRel, __builtin_fabsf(e)));
     c[j] = bits(uu);
   }
-  if (mx2 >= 0.5f) {  // a near-tie in the lane: the reference's divide for all 16
+  if (mx >= 0.5f) {  // a near-tie in the lane: the reference's divide for all 16
     const float* Qt = sqr + p * 64 + n0;
 #pragma unroll
     for (int j = 0; j < 16; j++) c[j] = (uint32_t)(int)roundf(Y[j] / Qt[(j >> 1) + 8 * (j & 1)]);
+  }
+  emit(c);
+}
+
+// Both in one pass (the fused encoder): the fast path, else the exact one.
+template <class Emit>
+__device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_t q, const float* sqr, int p,
+                                          Emit&& emit) {
+  uint32_t xr[4];
+  fdct_load(img, q, xr);
+  if (!fdct_fast(xr, tb, q, sqr, p, emit)) {
+    wave_sync();
+    fdct_exact(xr, tb, q, sqr, p, emit);
   }
 }
 
