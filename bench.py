@@ -5,7 +5,7 @@ Workloads (--workload; `auto`, the default, is chef-big at every rank count,
 so the driver's 1/2/4/8-GPU runs form one weak-scaling curve of one workload):
   chef-big  BASELINE.json configs[1], the metric's own configuration: a step
             is one DCT compress + decompress round trip of --inflight x
-            --batch (default 3 x 24 = 72) 4032x3008 IYUV frames per rank
+            --batch (default 4 x 24 = 96) 4032x3008 IYUV frames per rank
             (chef-with-trumpet-big, q=50; its raw input is missing from the
             reference, so the frame is the sha-pinned decode of
             chef-with-trumpet-big-DCT-50.myyuv), read from --input-frames
@@ -148,7 +148,7 @@ def parse(argv=None):
                     help="time the step without K1's HIP events (no roofline)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="launch groups in flight per GPU, each on its own codec context and HIP stream "
-                         "(1 = strictly serial; 0 = 3)")
+                         "(1 = strictly serial; 0 = 4)")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per launch (the batch entry points; 0 = 24)")
     ap.add_argument("--stream-priority", default="",
@@ -165,7 +165,7 @@ def parse(argv=None):
     ap.add_argument("--input-frames", type=int, default=0,
                     help="chef-big: distinct HBM copies of the input frame the launch groups read in turn "
                          "(0: one per frame of a step, at least 24; rounded down to a multiple of --batch: "
-                         "72 copies, 1.31 GB at the default 3 x 24, larger than the 256 MiB Infinity Cache)")
+                         "96 copies, 1.75 GB at the default 4 x 24, larger than the 256 MiB Infinity Cache)")
     ap.add_argument("--cpu-codec", action="store_true",
                     help="tests only: the CPU restatement as the codec, host tensors, gloo (no GPU)")
     ap.add_argument("--cpu-codec-fail", default="",
@@ -828,10 +828,12 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     name = args.workload if args.workload != "auto" else "chef-big"
     dist = None
-    # launch shape 3 x 24: the launch groups' overflow lists (~200k blocks) take the CAP-16 tier;
-    # chef-big driver shape 264.2k against 233.1k MP/s for 4 x 8 (two rounds, profiles/r3zzf_*, r3zzg_*,
-    # flat from 3 x 24 to 3 x 48), batch4k 263.0k against 243.3k (profiles/r3zzh_*)
-    nf = max(1, args.inflight or 3)
+    # launch shape 4 x 24: the launch groups' overflow lists (~200k blocks) take the CAP-16 tier
+    # (round 3: 3 x 24 264.2k against 233.1k MP/s for 4 x 8, flat from 3 x 24 to 3 x 48,
+    # profiles/r3zzf_*, r3zzg_*); with round 4's K1, 4 x 24 288.1k / 292.2k against 3 x 24
+    # 282.6k / 287.0k at 20 / 40 steps, 5 streams slower (one per hardware queue: 4),
+    # profiles/r4j_launch_shapes.txt
+    nf = max(1, args.inflight or 4)
     prios = [int(v) for v in args.stream_priority.split(",")] if args.stream_priority else [0]
     big = myyuv_file.YUVFile.load(GOLDEN_BIG)
     if args.cpu_codec:

@@ -116,16 +116,17 @@ int myyuv_gpu_dct_decompress_device(myyuv_hip_handle h, const void* d_payload,
  * of frame f > 0 reports f * blocks_per_frame.  Each frame's bytes are those
  * of the single-frame call.
  * Workspace (myyuv_hip_reserve_batch reserves it up front; the calls grow it
- * on demand): about 466 B per 8x8 block of the batch — the encoder's stage
+ * on demand): about 471 B per 8x8 block of the batch — the encoder's stage
  * (160 B: a tile's chunks, kMaxChunk per block, rounded up to whole 4-tile
  * K2 windows) and overflow slots (160 B per block: any block may exceed 8
  * distinct symbols, as nearly all of a noise frame's do, so the slots cannot
  * be sized from a typical list), the coefficients (128 B), the chunk offsets
  * (u32 srcoff, 4 B), the decoder's group offsets (4 B), the overflow worklist
  * (8 B: the CAP-16 tier's list and its rest list), the sizes and row masks
- * (2 B).  A 4032x3008 frame (284,256 blocks) takes ~132 MB: the bench's
- * 24-frame launch groups ~3.2 GB per context, 3 contexts ~9.5 GB; a 16-frame
- * 8192x8192 batch ~11.7 GB (of 288 GB). */
+ * (2 B), K1's per-block words for K2 (4 B) and its exact-path list (0.25 B).
+ * A 4032x3008 frame (284,256 blocks) takes ~134 MB: the bench's 24-frame
+ * launch groups ~3.2 GB per context, 3 contexts ~9.6 GB; a 16-frame
+ * 8192x8192 batch ~11.9 GB (of 288 GB). */
 int myyuv_hip_reserve_batch(myyuv_hip_handle h, uint32_t width, uint32_t height, uint32_t nframes);
 int myyuv_gpu_dct_compress_batch_device(myyuv_hip_handle h, const void* d_iyuv, uint32_t nframes,
                                         uint32_t width, uint32_t height, const uint8_t quality[3],
@@ -181,7 +182,8 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
 #define MYYUV_K_HUFF_WAVE 9  /* K2 overflow pass, wave per block (short worklists) */
 #define MYYUV_K_BMP 10       /* K7 bmp_to_iyuv (BMP -> IYUV conversion) */
 #define MYYUV_K_FDCT_FIX 11  /* K1's exact path for the units K1 listed (fdct_fix) */
-#define MYYUV_K_COUNT 12
+#define MYYUV_K_IDCT_FIX 12  /* the fused decoder's exact path for the blocks it listed (idct_fix) */
+#define MYYUV_K_COUNT 13
 int myyuv_hip_profile(myyuv_hip_handle h, int enable);
 /* As myyuv_hip_profile, but stamps only the kernels whose bit (1 << MYYUV_K_*)
  * is set in `mask` (0 disables): event stamping costs host and queue time per

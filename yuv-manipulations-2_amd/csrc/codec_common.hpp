@@ -14,6 +14,13 @@ constexpr uint32_t kXfUnit = 16;  // blocks per K1/K6 wave unit (four lanes per 
 #endif
 constexpr uint32_t kXfWaves = MYYUV_XF_WAVES;  // persistent K1/K6 grid: waves (8 per SIMD)
 constexpr int kSlotWords = 40;  // 160-B chunk slot per block (max chunk 155 B)
+// K1/K6 sink (stores of lanes past a plane's end and of all-zero rows):
+// kSinkQuads 16-B words per slot, kSinkSlots slots, wave w using slot
+// w % kSinkSlots (one slot: every wave's skipped stores meet in 3 KB)
+#ifndef MYYUV_SINK_SLOTS
+#define MYYUV_SINK_SLOTS 1
+#endif
+constexpr uint32_t kSinkQuads = 192, kSinkSlots = MYYUV_SINK_SLOTS;
 constexpr int kMaxChunk = 160;
 
 // Float-literal DCT-II basis, row u = basis u (DCT.cpp:221-230).  Literal
@@ -41,6 +48,37 @@ constexpr int kMaxChunk = 160;
   {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,    \
    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,    \
    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63}
+
+// K2 block classes (k_huff_encode sorts a window's blocks by class so each
+// wave runs the cheapest encoder that fits all its blocks):
+//   single: msz <= 1, one symbol;  r4 / r8: at most 4 / 8 distinct symbols
+//   for sure (nonzero coefficients, plus one for a zero inside the message);
+//   r8x: the rest, encode_block_r<8> with the overflow worklist behind it.
+// msz = 1 + zig-zag index of the last nonzero coefficient (0: all zero).
+constexpr uint32_t kClassSingle = 0, kClassR4 = 1, kClassR8 = 2, kClassR8x = 3, kClassDead = 4;
+__host__ __device__ __forceinline__ uint32_t class_of(uint32_t nnz, uint32_t msz) {
+  if (msz <= 1) return kClassSingle;
+  const uint32_t nub = nnz + (msz > nnz ? 1u : 0u);
+  return nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
+}
+// Natural coefficient pair w (coefficients 2w, 2w+1): (zig-zag index + 1) of
+// each, in the two 16-bit halves.
+struct ZzPairs {
+  uint32_t v[32];
+  constexpr ZzPairs() : v{} {
+    constexpr uint8_t zz[64] = MYYUV_ZIGZAG;
+    uint32_t inv[64] = {};
+    for (int i = 0; i < 64; i++) inv[zz[i]] = (uint32_t)i + 1u;
+    for (int w = 0; w < 32; w++) v[w] = inv[2 * w] | (inv[2 * w + 1] << 16);
+  }
+};
+constexpr ZzPairs kZzPairs{};
+// K1 -> K2 per-block word (binfo): bits 0-7 the row mask, 8-14 msz, 15-17 the
+// class, 18-28 the DC coefficient's low 11 bits (all K2's classification
+// needs: it reads 4 B per block instead of the coefficient rows).
+__host__ __device__ __forceinline__ uint32_t binfo_word(uint32_t rm, uint32_t msz, uint32_t cls, uint32_t dc) {
+  return rm | (msz << 8) | (cls << 15) | ((dc & 0x7FFu) << 18);
+}
 
 // Geometry of one IYUV frame as the kernels see it.  Blocks are numbered
 // globally plane-major (Y, U, V), row-major inside a plane, which is the

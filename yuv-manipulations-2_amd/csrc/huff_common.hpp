@@ -642,19 +642,12 @@ MYYUV_HD void emit_chunk(const EncState& S, int wave_msz, W& bw) {
   }
 }
 
-// K2 block classes (k_huff_encode sorts a workgroup's blocks by class so each
-// wave runs the cheapest encoder that fits all its blocks):
-//   single: msz <= 1, one symbol;  r4 / r8: at most 4 / 8 distinct symbols
-//   for sure (nonzero coefficients, plus one for a zero inside the message);
-//   r8x: the rest, encode_block_r<8> with the overflow worklist behind it.
-constexpr uint32_t kClassSingle = 0, kClassR4 = 1, kClassR8 = 2, kClassR8x = 3, kClassDead = 4;
+// K2 block classes: class_of (codec_common.hpp) from the nonzero count and msz.
 MYYUV_HD uint32_t block_class(const CoefRegs& R, int msz) {
-  if (msz <= 1) return kClassSingle;
   uint32_t nnz = 0;
 #pragma unroll
   for (int w = 0; w < 32; w++) nnz += ((R.w[w] & 0xFFFFu) != 0) + ((R.w[w] >> 16) != 0);
-  const uint32_t nub = nnz + ((uint32_t)msz > nnz ? 1u : 0u);
-  return nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
+  return class_of(nnz, (uint32_t)msz);
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -664,15 +657,6 @@ MYYUV_HD uint32_t block_class(const CoefRegs& R, int msz) {
 // index + 1) (v_pk_max_u16): five instructions per pair where the scalar
 // forms take about ten.  Same results as the host forms.
 typedef unsigned short myyuv_us2 __attribute__((ext_vector_type(2)));
-struct ZzPairs {
-  uint32_t v[32];  // natural pair w: (zig-zag index + 1) of coefficients 2w, 2w+1
-  constexpr ZzPairs() : v{} {
-    uint32_t inv[64] = {};
-    for (int i = 0; i < 64; i++) inv[c_zz[i]] = (uint32_t)i + 1u;
-    for (int w = 0; w < 32; w++) v[w] = inv[2 * w] | (inv[2 * w + 1] << 16);
-  }
-};
-constexpr ZzPairs kZzPairs{};
 __device__ __forceinline__ void block_class_msz(const CoefRegs& R, int& msz, uint32_t& cls) {
   myyuv_us2 cnt = {0, 0}, mx = {0, 0};
 #pragma unroll
@@ -693,12 +677,7 @@ __device__ __forceinline__ void block_class_msz(const CoefRegs& R, int& msz, uin
   const uint32_t nnz = (uint32_t)cnt.x + (uint32_t)cnt.y;
   const int m = (int)(mx.x > mx.y ? mx.x : mx.y);
   msz = m;
-  if (m <= 1) {
-    cls = kClassSingle;
-  } else {
-    const uint32_t nub = nnz + ((uint32_t)m > nnz ? 1u : 0u);
-    cls = nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
-  }
+  cls = class_of(nnz, (uint32_t)m);
 }
 #else
 MYYUV_HD void block_class_msz(const CoefRegs& R, int& msz, uint32_t& cls) {

@@ -1037,7 +1037,7 @@ struct WinScratch {
 #define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (12 spilled; 6 measured +1.5 % before the emit tables, −1 % after: its spills grew; tools/ab_bench.sh, tools/kus_ab.sh)
 #endif
 __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
-                                                         const uint8_t* __restrict__ rmask,
+                                                         const uint32_t* __restrict__ binfo,
                                                          const uint4* __restrict__ zq, FrameGeom G,
                                                          uint32_t* __restrict__ stage,
                                                          uint32_t* __restrict__ tinfo,
@@ -1077,29 +1077,20 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     sc.done = 0;
     sc.ntl = min(kWinTiles, NT - T0);
   }
-  // ---- 1. classify, with per-round ballot ranks
+  // ---- 1. classify from K1's per-block words (row mask, msz, class, DC;
+  // 4 B per block, coalesced), with per-round ballot ranks
   uint32_t ent[kWinTiles];  // per round: class | msz << 3 | row mask << 10 | rank << 18
-  uint32_t rmv[kWinTiles];
+  uint32_t biv[kWinTiles];
 #pragma unroll
-  for (uint32_t k = 0; k < kWinTiles; k++) rmv[k] = tid < nlk[k] ? rmask[gbk[k] + tid] : 0u;
-  // round k + 1's coefficients are loaded before round k is classified
-  CoefRegs RR[2];
-  RR[0].load(coef, zq, tid < nlk[0] ? gbk[0] + tid : 0u, rmv[0]);
+  for (uint32_t k = 0; k < kWinTiles; k++) biv[k] = tid < nlk[k] ? binfo[gbk[k] + tid] : 0u;
 #pragma unroll
   for (uint32_t k = 0; k < kWinTiles; k++) {
-    if (k + 1 < kWinTiles)
-      RR[(k + 1) & 1].load(coef, zq, tid < nlk[(k + 1) % kWinTiles] ? gbk[(k + 1) % kWinTiles] + tid : 0u,
-                           rmv[(k + 1) % kWinTiles]);
-    uint32_t cls = kClassDead, m = 0;
-    const uint32_t rm = rmv[k];
-    if (tid < nlk[k]) {
-      int msz;
-      block_class_msz(RR[k & 1], msz, cls);
-      m = (uint32_t)msz;
-    }
+    const uint32_t bi = biv[k];
+    const uint32_t cls = tid < nlk[k] ? (bi >> 15) & 7u : kClassDead;
+    const uint32_t m = (bi >> 8) & 127u, rm = bi & 0xFFu;
     const uint32_t key = sort_key(cls, m);
 #if MYYUV_K2_DC_LDS
-    sc.dc[(k << 8) | tid] = (uint16_t)RR[k & 1].w[0];  // (masked rows were loaded as zeros)
+    sc.dc[(k << 8) | tid] = (uint16_t)(bi >> 18);  // the DC's low 11 bits (build_single_dc uses those)
 #endif
     uint32_t rk = 0;
 #pragma unroll

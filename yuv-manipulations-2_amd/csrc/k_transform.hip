@@ -79,6 +79,12 @@
 #else
 #define MYYUV_XF_ATTR
 #endif
+// K1: 8 waves per SIMD (its LDS allows 8 workgroups per CU); the compiler
+// otherwise settles at 69 VGPRs (7 waves) with the block-info computation
+#ifndef MYYUV_K1_OCC
+#define MYYUV_K1_OCC 8
+#endif
+#define MYYUV_K1_ATTR __attribute__((amdgpu_waves_per_eu(MYYUV_K1_OCC, MYYUV_K1_OCC)))
 
 namespace myyuv_gpu {
 
@@ -86,15 +92,20 @@ using namespace xf;
 
 // K1: u8 planes -> int16 coefficients (natural order, quad layout).
 // DCT.cpp:297-306 (gather, x - 128), :269-277 (applyDCTBlock).
-// Rows 2q, 2q+1 of lane (b, q)'s block (coefficient quads 2q, 2q+1) and the
-// block's row mask for K2 (bit c: row c has a nonzero coefficient, from the
-// block's four lanes).  An all-zero row is not stored (K2 reads masked-off
-// rows from a zero buffer), which saves most of the 128 B per block of a
-// q=50 frame twice (this write, K2's read).  Every lane still issues its three
-// stores (the sink takes the skipped ones and those of lanes past the
-// plane's end).
+typedef unsigned short k1_us2 __attribute__((ext_vector_type(2)));
+
+// Rows 2q, 2q+1 of lane (b, q)'s block (coefficient quads 2q, 2q+1), the
+// block's row mask (bit c: row c has a nonzero coefficient, from the block's
+// four lanes) and its K2 info word (binfo_word: row mask, msz, class, DC),
+// which lets K2 classify its blocks from 4 B each instead of their rows.  An
+// all-zero row is not stored (K2 reads masked-off rows from a zero buffer),
+// which saves most of the 128 B per block of a q=50 frame twice (this write,
+// K2's read).  Every lane still issues its four stores (the sink takes the
+// skipped ones and those of lanes past the plane's end).  zq: the lane's
+// eight (zig-zag index + 1) pairs, kZzPairs.v[8q .. 8q+7].
 __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32_t q, uint32_t lane, bool live,
                                                  uint32_t g, uint4* dlo, uint4* dhi, uint8_t* __restrict__ rmask,
+                                                 uint32_t* __restrict__ binfo, const uint4* zq,
                                                  uint4* __restrict__ sink) {
   uint4 lo, hi;
   uint32_t rm;
@@ -105,11 +116,45 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
     *dhi = hi;
   }
 #else
+  // nonzero count and msz of the lane's natural pairs 8q .. 8q+7 (lo: row
+  // 2q, hi: row 2q+1) in packed 16-bit arithmetic, as K2's block_class_msz:
+  // flag = min(v, 1) per half, count += flag, max of (0 - flag) & (index + 1)
+  const uint4 z0 = zq[0], z1 = zq[1];
+  const uint32_t wv[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t zv[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+  k1_us2 cnt = {0, 0}, mx = {0, 0};
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t fu, m16;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(fu) : "v"(wv[i]), "s"(0x00010001u));
+    cnt += __builtin_bit_cast(k1_us2, fu);
+    asm("v_pk_sub_u16 %0, 0, %1" : "=v"(m16) : "v"(fu));
+    mx = __builtin_elementwise_max(mx, __builtin_bit_cast(k1_us2, m16 & zv[i]));
+  }
+  // the block's four lanes: counts add, msz is the maximum (one shuffle per
+  // step carries both)
+  uint32_t nnz = (uint32_t)cnt.x + (uint32_t)cnt.y;
+  uint32_t msz = mx.x > mx.y ? (uint32_t)mx.x : (uint32_t)mx.y;
+#pragma unroll
+  for (int d = 1; d < 4; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)(nnz | (msz << 16)), d, 64);
+    nnz += o & 0xFFFFu;
+    msz = max(msz, o >> 16);
+  }
   const bool nzl = (rm >> (2 * q)) & 1u, nzh = (rm >> (2 * q + 1)) & 1u;
   *(live ? rmask + g : reinterpret_cast<uint8_t*>(sink + 128) + lane) = (uint8_t)rm;
+  // the block's four lanes store the same word (lane 4b holds row 0: the DC
+  // is the low half of its lo.x)
+  const uint32_t dc = (uint32_t)__shfl((int)lo.x, (int)(lane & ~3u), 64);
+  *(live ? binfo + g : reinterpret_cast<uint32_t*>(sink + 132) + lane) = binfo_word(rm, msz, class_of(nnz, msz), dc);
   *(nzl ? dlo : sink + lane) = lo;
   *(nzh ? dhi : sink + 64 + lane) = hi;
 #endif
+}
+
+// The zig-zag pair table in LDS (kZzPairs; before the tables' barrier)
+__device__ __forceinline__ void stage_zz(uint4* szz) {
+  if (threadIdx.x < 32) reinterpret_cast<uint32_t*>(szz)[threadIdx.x] = kZzPairs.v[threadIdx.x];
 }
 
 // K1's exact path out of line (MYYUV_K1_INLINE_EXACT 0): a unit whose fast
@@ -121,11 +166,12 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
 #define MYYUV_K1_INLINE_EXACT 0
 #endif
 
-__global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t* __restrict__ frame, FrameGeom G,
+__global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t* __restrict__ frame, FrameGeom G,
                                                    const QTables* __restrict__ qt,
                                                    uint4* __restrict__ coef, uint8_t* __restrict__ rmask,
-                                                   uint4* __restrict__ sink, uint32_t* __restrict__ k2ctl,
-                                                   uint32_t* __restrict__ fix, uint32_t par) {
+                                                   uint32_t* __restrict__ binfo, uint4* __restrict__ sink,
+                                                   uint32_t* __restrict__ k2ctl, uint32_t* __restrict__ fix,
+                                                   uint32_t par) {
 #if MYYUV_K1_PRIO > 0
   // wave issue priority over the other launch groups' kernels on the SIMD
   __builtin_amdgcn_s_setprio(MYYUV_K1_PRIO);
@@ -134,8 +180,11 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
   if (k2ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *k2ctl = 0u;
   __shared__ float tile[4][kXfUnit * kTile];
   __shared__ float sqr[2 * 3 * 64];  // QTables::q then QTables::r
+  __shared__ uint4 szz[8];
   static_assert(offsetof(QTables, r) == sizeof(float) * 3 * 64, "layout");
+  stage_zz(szz);
   stage_tables<2 * 3 * 64>(qt->q[0], sqr);
+  if (kSinkSlots > 1) sink += (size_t)((blockIdx.x * 4u + (threadIdx.x >> 6)) % kSinkSlots) * kSinkQuads;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t q = lane & 3u, b = lane >> 2;  // quarter, block in the unit
   float* tb = tile[threadIdx.x >> 6] + b * kTile;
@@ -186,7 +235,9 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
     }
     continue;
 #endif
-    auto store = [&](const uint32_t (&c)[16]) { store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, sink); };
+    auto store = [&](const uint32_t (&c)[16]) {
+      store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
+    };
 #if MYYUV_K1_INLINE_EXACT
     fdct_core(img, tb, q, sqr, U.p, store);
 #else
@@ -203,13 +254,16 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_fdct_quant(const uint8_t*
 // previous fix launch, its reader, is done: stream order).
 __global__ __launch_bounds__(256) void k_fdct_fix(const uint8_t* __restrict__ frame, FrameGeom G,
                                                   const QTables* __restrict__ qt, uint4* __restrict__ coef,
-                                                  uint8_t* __restrict__ rmask, uint4* __restrict__ sink,
+                                                  uint8_t* __restrict__ rmask, uint32_t* __restrict__ binfo,
+                                                  uint4* __restrict__ sink,
                                                   uint32_t* __restrict__ fix, uint32_t par) {
   __shared__ float tile[4][kXfUnit * kTile];
   __shared__ float sqr[2 * 3 * 64];
+  __shared__ uint4 szz[8];
   if (blockIdx.x == 0 && threadIdx.x == 0) fix[par ^ 1u] = 0u;
   const uint32_t n = __builtin_amdgcn_readfirstlane(fix[par]);
   if (blockIdx.x * 4u >= n) return;  // (uniform over the workgroup)
+  stage_zz(szz);
   stage_tables<2 * 3 * 64>(qt->q[0], sqr);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t q = lane & 3u, b = lane >> 2;
@@ -232,7 +286,9 @@ __global__ __launch_bounds__(256) void k_fdct_fix(const uint8_t* __restrict__ fr
     uint32_t xr[4];
     fdct_load(img, q, xr);
     fdct_exact(xr, tb, q, sqr, U.p,
-               [&](const uint32_t (&c)[16]) { store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, sink); });
+               [&](const uint32_t (&c)[16]) {
+                 store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
+               });
   }
 }
 

@@ -27,16 +27,17 @@
 #endif
 
 namespace myyuv_gpu {
-__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*,
-                             uint32_t*, uint32_t);
-__global__ void k_fdct_fix(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint4*, uint32_t*,
-                           uint32_t);
+__global__ void k_fdct_quant(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint32_t*, uint4*,
+                             uint32_t*, uint32_t*, uint32_t);
+__global__ void k_fdct_fix(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint32_t*, uint4*,
+                           uint32_t*, uint32_t);
 __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*,
                                uint4*);
 __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*, const uint32_t*,
                               const uint32_t*, FrameGeom, uint32_t, uint32_t, const QTables*, uint4*, uint8_t*,
-                              unsigned long long*);
-__global__ void k_huff_encode(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
+                              unsigned long long*, uint32_t*, uint32_t);
+__global__ void k_idct_fix(const uint4*, FrameGeom, const QTables*, uint8_t*, uint32_t*, uint32_t);
+__global__ void k_huff_encode(const uint4*, const uint32_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
                               uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
                                    const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t,
@@ -187,11 +188,12 @@ struct myyuv_hip_ctx {
   DevBuf stage, oslots, tinfo, srcoff;  // K2 -> K4 (codec_common.hpp)
   DevBuf bmp;   // staged BMP pixels (host-buffer BMP -> IYUV)
   DevBuf bsizes;  // u32 payload sizes of a host-buffer batch
-  DevBuf rmask; // per block: bit c = coefficient row c nonzero (K5 -> K6)
+  DevBuf rmask; // per block: bit c = coefficient row c nonzero (K1 -> overflow passes, K5 -> K6)
+  DevBuf binfo; // per block: K1 -> K2's classification (binfo_word, codec_common.hpp)
   DevBuf zq;    // 256 zero bytes: K6's source for rows the mask says are zero
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
-  // K1 -> k_fdct_fix: [0], [1] the unit counts of even / odd launches
-  // (fix_par), from [64] the units
+  // K1 -> k_fdct_fix and k_decode_idct -> k_idct_fix: [0], [1] the counts of
+  // even / odd launches (fix_par), from [64] the listed units / blocks
   DevBuf fix;
   uint32_t fix_par = 0;
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
@@ -335,6 +337,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->srcoff.grow((size_t)nblk * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
   e |= c->rmask.grow((size_t)nblk);
+  e |= c->binfo.grow((size_t)nblk * 4);
   if (c->zq.n == 0) {
     e |= c->zq.grow(256);
     if (!e && hipMemset(c->zq.p, 0, 256) != hipSuccess) e |= MYYUV_E_HIP;
@@ -342,13 +345,13 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->loff.grow((size_t)nblk * 4);
   e |= c->tiles.grow((size_t)nf * (ntiles + 1) * 4);
   e |= c->err.grow(8);
-  e |= c->sink.grow(192 * 16);  // K1/K6: 2 x 64 quads + K1's 64 mask bytes
+  e |= c->sink.grow((size_t)kSinkQuads * 16 * kSinkSlots);  // K1/K6: 2 x 64 quads + K1's 64 mask bytes + 64 words
   e |= c->psize.grow(4);
   e |= c->desc.grow((size_t)nf * sizeof(StreamDesc));
   // [0], [1]: overflow counts, then K2's list and (single frames) the CAP-16 tier's (launch_overflow)
   e |= c->work.grow((size_t)nblk * (nf == 1 || MYYUV_R16_BATCH ? 8 : 4) + 256);
   {
-    const size_t fb = ((size_t)G.ucum[3] * nf + 64) * 4;
+    const size_t fb = ((size_t)nblk + 64) * 4;
     if (c->fix.n < fb) {
       e |= c->fix.grow(fb);
       if (!e && (hipMemset(c->fix.p, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
@@ -390,7 +393,7 @@ int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   uint32_t* list = count + 64;
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
   const int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(win_tiles_alloc(nf * G.tcum[3]) / kWinTiles), dim3(kK2Group), s,
-               c->coef.as<const uint4>(), c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G,
+               c->coef.as<const uint4>(), c->binfo.as<const uint32_t>(), c->zq.as<const uint4>(), G,
                c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
                c->srcoff.as<uint32_t>(), list, count);
   return e | launch_overflow(c, G, s);
@@ -443,15 +446,15 @@ int launch_fdct(myyuv_hip_ctx* c, const FrameGeom& G, const uint8_t* in, const Q
   const uint32_t par = c->fix_par;
   c->fix_par ^= 1u;
   int e = launch(c, MYYUV_K_FDCT, k_fdct_quant, xf_grid(G, c->xf_resident[0]), dim3(256), s, in, G, qt,
-                 c->coef.as<uint4>(), c->rmask.as<uint8_t>(), c->sink.as<uint4>(), k2ctl, c->fix.as<uint32_t>(),
-                 par);
+                 c->coef.as<uint4>(), c->rmask.as<uint8_t>(), c->binfo.as<uint32_t>(), c->sink.as<uint4>(), k2ctl,
+                 c->fix.as<uint32_t>(), par);
   uint32_t qmax = 0;
   for (int p = 0; p < 3; p++) qmax = std::max(qmax, (uint32_t)c->q_cached[p]);
   const uint32_t want =
       (c->fix_grid == 0 || !c->q_valid || qmax > c->fix_qmax) ? c->fix_resident : c->fix_grid;
   const uint32_t grid = std::max(1u, std::min(want, ceil_div(G.ucum[3] * G.nframes, 4)));
   e |= launch(c, MYYUV_K_FDCT_FIX, k_fdct_fix, dim3(grid), dim3(256), s, in, G, qt, c->coef.as<uint4>(),
-              c->rmask.as<uint8_t>(), c->sink.as<uint4>(), c->fix.as<uint32_t>(), par);
+              c->rmask.as<uint8_t>(), c->binfo.as<uint32_t>(), c->sink.as<uint4>(), c->fix.as<uint32_t>(), par);
   return e;
 }
 
@@ -509,9 +512,17 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
                  t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
   if (c->fused_dec) {  // K5 + K6 in one pass, the coefficients kept on chip
+    const uint32_t par = c->fix_par;
+    c->fix_par ^= 1u;
     e |= launch(c, MYYUV_K_HUFF_DEC, k_decode_idct, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size, cap,
                 (const StreamDesc*)desc, c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
-                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err);
+                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err, c->fix.as<uint32_t>(), par);
+    // the blocks whose fast-path pixels are not proven (1.6 % of the bench
+    // frame's blocks with an AC coefficient, tools/diag/fast_idct_sim.py):
+    // 64 per workgroup
+    const uint32_t grid = std::max(1u, std::min(c->fix_resident, ceil_div(nblk * nf, 64u * 16u)));
+    e |= launch(c, MYYUV_K_IDCT_FIX, k_idct_fix, dim3(grid), dim3(256), s, c->coef.as<const uint4>(), G, qt,
+                static_cast<uint8_t*>(d_out), c->fix.as<uint32_t>(), par);
     return e ? MYYUV_E_HIP : 0;
   }
   e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size,
@@ -688,7 +699,7 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   (void)hipEventDestroy(c->done);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->stage, &c->oslots, &c->tinfo, &c->srcoff, &c->sizes, &c->loff, &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
-                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes};
+                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes, &c->fix, &c->binfo};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1142,14 +1153,26 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
   if (reserve(c, G)) return MYYUV_E_HIP;
   const uint32_t nwaves = ceil_div(nblocks, kWave);
   // host-side relayout into K1's output format: natural-order quads
-  std::vector<uint32_t> words((size_t)nwaves * kCoefQuadsPerWave * 4, 0u);
+  // and the per-block words K1 writes for K2's classification (binfo_word;
+  // every row marked present)
+  std::vector<uint32_t> words((size_t)nwaves * kCoefQuadsPerWave * 4, 0u), info(nblocks);
   for (uint32_t g = 0; g < nblocks; g++) {
     int16_t nat[64];
-    for (int z = 0; z < 64; z++) nat[kZigzag[z]] = coef_zz[(size_t)g * 64 + z];
+    uint32_t nnz = 0, msz = 0;
+    for (int z = 0; z < 64; z++) {
+      const int16_t v = coef_zz[(size_t)g * 64 + z];
+      nat[kZigzag[z]] = v;
+      if (v != 0) {
+        nnz++;
+        msz = (uint32_t)z + 1u;
+      }
+    }
     for (uint32_t c4 = 0; c4 < 8; c4++)
       std::memcpy(&words[(size_t)coef_quad(g, c4) * 4], nat + 8 * c4, 16);
+    info[g] = binfo_word(0xFFu, msz, class_of(nnz, msz), (uint32_t)(uint16_t)nat[0]);
   }
   if (hipMemcpy(c->coef.p, words.data(), words.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->binfo.p, info.data(), (size_t)nblocks * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemsetAsync(c->rmask.p, 0xFF, nblocks, s) != hipSuccess ||  // every row present
       hipMemsetAsync(c->work.p, 0, 4, s) != hipSuccess)  // K1 zeroes it in the codec path
     return MYYUV_E_HIP;
