@@ -182,8 +182,7 @@ int myyuv_hip_sync_status(myyuv_hip_handle h, void* stream, int64_t* bad_block);
 #define MYYUV_K_HUFF_WAVE 9  /* K2 overflow pass, wave per block (short worklists) */
 #define MYYUV_K_BMP 10       /* K7 bmp_to_iyuv (BMP -> IYUV conversion) */
 #define MYYUV_K_FDCT_FIX 11  /* K1's exact path for the units K1 listed (fdct_fix) */
-#define MYYUV_K_IDCT_FIX 12  /* the fused decoder's exact path for the blocks it listed (idct_fix) */
-#define MYYUV_K_COUNT 13
+#define MYYUV_K_COUNT 12
 int myyuv_hip_profile(myyuv_hip_handle h, int enable);
 /* As myyuv_hip_profile, but stamps only the kernels whose bit (1 << MYYUV_K_*)
  * is set in `mask` (0 disables): event stamping costs host and queue time per

@@ -49,15 +49,6 @@ constexpr uint32_t kStageQuads = 384;
 // the value needs no select.
 constexpr uint32_t kZeroBit = kStageQuads * 128u;
 
-// the fused decoder's transform: the fast inverse with a per-output proof and
-// k_idct_fix behind it (1), or the reference's order throughout (0)
-#ifndef MYYUV_DEC_FAST
-#define MYYUV_DEC_FAST 0
-#endif
-#ifndef MYYUV_DEC_FIXLIST
-#define MYYUV_DEC_FIXLIST 1  // (0: tuning builds only, unproven blocks not fixed)
-#endif
-
 // diagnostic ablations (never the product): 1 = no symbol decode, 2 = no
 // table parse either, 3 = the fused decoder skips its transform
 #ifndef MYYUV_K5_EXP
@@ -506,14 +497,9 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
                                                    uint32_t tiles_p1, const QTables* __restrict__ qt,
                                                    uint4* __restrict__ coef,
                                                    uint8_t* __restrict__ frame,
-                                                   unsigned long long* __restrict__ err,
-                                                   uint32_t* __restrict__ fix, uint32_t par) {
+                                                   unsigned long long* __restrict__ err) {
   static_assert(sizeof(uint4) * kStageQuads >= sizeof(float) * xf::kXfTile16, "the tile over the stage");
-  // the stage, then (after the decode) the transpose tile and, behind it, the
-  // unit's 16 coefficient images (kept through the fast transform)
-  constexpr uint32_t kImgQuad = xf::kXfTile16 / 4;
-  static_assert(kImgQuad + 16 * 8 >= kStageQuads + 1, "the images end past the zero quad");
-  __shared__ uint4 stq[kImgQuad + 16 * 8];
+  __shared__ uint4 stq[kStageQuads + 1];
   __shared__ float sq[64];
   __shared__ uint16_t s_blk[64];
   const uint32_t lane = threadIdx.x;
@@ -607,23 +593,6 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     // (< 16) is zeroed by lane `lane` whether or not that lane also writes a
     // compacted block: the two slots differ (rrank < nrest <= 16u + lane).
     const bool mine = D.live && !isdc && (rrank >> 4) == u;
-#if MYYUV_DEC_FAST
-    uint4* const s_im = stq + kImgQuad;  // block slot k: quads 8k .. 8k+7
-    if (mine) {
-      uint4* img = s_im + 8u * (rrank & 15u);
-#pragma unroll
-      for (int c = 0; c < 8; c++) img[c] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
-    }
-    if (lane < 16u && 16u * u + lane >= nrest) {
-      uint4* img = s_im + 8u * lane;
-#pragma unroll
-      for (int c = 0; c < 8; c++) img[c] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    xf::wave_sync();
-    uint2 w0, w1;
-    const bool lfail =
-        xf::idct_rows_fast(reinterpret_cast<const uint32_t*>(s_im + 8u * b), tile + b * xf::kTile, q, sq, w0, w1);
-#else
     if (mine) {
       uint4* img = reinterpret_cast<uint4*>(tile + (rrank & 15u) * xf::kTile);
 #pragma unroll
@@ -637,82 +606,13 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     xf::wave_sync();
     uint2 w0, w1;
     xf::idct_rows(tile + b * xf::kTile, q, sq, w0, w1);
-#endif
-    const bool blive = 16u * u + b < nrest;
-    const uint32_t gl = D.g0 + s_blk[(16u * u + b) & 63u];  // the block of compacted position 16u + b
-    if (blive) {
+    if (16u * u + b < nrest) {
+      const uint32_t gl = D.g0 + s_blk[16u * u + b];  // the block of compacted position 16u + b
       const uint32_t off = xf::block_row_offset(U, gl - U.cum, 2u * q);
       *reinterpret_cast<uint2*>(fr + off) = w0;
       *reinterpret_cast<uint2*>(fr + off + U.pw) = w1;
     }
-#if MYYUV_DEC_FAST
-    // blocks with an unproven pixel: their four lanes copy the block's image
-    // (natural quads) to coef, lane q = 0 lists the block for k_idct_fix
-    const uint64_t fl = __ballot(lfail && blive);
-    if (MYYUV_DEC_FIXLIST && fl) {
-      const bool bfail = ((fl >> (4u * b)) & 0xFull) != 0;
-      const uint32_t gg = D.gbase + gl;
-      if (bfail) {
-        coef[coef_quad(gg, 2 * q)] = s_im[8u * b + 2 * q];
-        coef[coef_quad(gg, 2 * q + 1)] = s_im[8u * b + 2 * q + 1];
-      }
-      const uint64_t lm = __ballot(bfail && q == 0);
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(fix + par, (uint32_t)__popcll(lm));
-      base = __builtin_amdgcn_readfirstlane(base);
-      if (bfail && q == 0) fix[64 + base + (uint32_t)__popcll(lm & ((1ull << lane) - 1ull))] = gg;
-    }
-#endif
     xf::wave_sync();  // the next unit rewrites the tile
-  }
-}
-
-// The fused decoder's exact path for the blocks it listed (fix[par] of them,
-// batch-global block indices at fix + 64; their coefficients in coef as
-// natural quads): 16 blocks per wave, four lanes per block, idct_rows in the
-// reference's order, the pixel rows over the fast path's.  Workgroup 0 zeroes
-// the other parity's count for the next producer (stream order).
-__global__ __launch_bounds__(256) void k_idct_fix(const uint4* __restrict__ coef, FrameGeom G,
-                                                  const QTables* __restrict__ qt, uint8_t* __restrict__ frame,
-                                                  uint32_t* __restrict__ fix, uint32_t par) {
-  __shared__ float tile[4][xf::kXfTile16];
-  __shared__ float sq[3 * 64];
-  if (blockIdx.x == 0 && threadIdx.x == 0) fix[par ^ 1u] = 0u;
-  const uint32_t n = __builtin_amdgcn_readfirstlane(fix[par]);
-  if (blockIdx.x * 64u >= n) return;  // (uniform over the workgroup)
-  for (uint32_t i = threadIdx.x; i < 3u * 64u; i += 256u) sq[i] = qt->q[0][i];
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u, q = lane & 3u, b = lane >> 2;
-  float* tb = tile[threadIdx.x >> 6] + b * xf::kTile;
-  const uint32_t w0i = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
-  for (uint32_t i0 = 16u * w0i; i0 < n; i0 += 16u * nw) {
-    const bool live = i0 + b < n;
-    const uint32_t gg = fix[64 + (live ? i0 + b : i0)];
-    const uint32_t f = gg / G.cum[3], gl = gg - f * G.cum[3];
-    const int p = gl >= G.cum[1] ? (gl >= G.cum[2] ? 2 : 1) : 0;
-    // the block's image: quads 2q, 2q+1 by lane q
-    xf::wave_sync();  // (the previous round's tile reads are done)
-    uint4* img = reinterpret_cast<uint4*>(tb);
-    img[2 * q] = coef[coef_quad(gg, 2 * q)];
-    img[2 * q + 1] = coef[coef_quad(gg, 2 * q + 1)];
-    xf::wave_sync();
-    uint2 r0, r1;
-    xf::idct_rows(tb, q, sq + p * 64, r0, r1);
-    if (live) {
-      xf::Unit U;
-      U.p = p;
-      U.cum = G.cum[p];
-      U.nb = G.cum[p + 1] - G.cum[p];
-      U.poff = p == 0 ? G.poff[0] : (p == 1 ? G.poff[1] : G.poff[2]);
-      U.pw = p == 0 ? G.pw[0] : (p == 1 ? G.pw[1] : G.pw[2]);
-      U.bw = p == 0 ? G.bw[0] : (p == 1 ? G.bw[1] : G.bw[2]);
-      U.bmag = p == 0 ? G.bmag[0] : (p == 1 ? G.bmag[1] : G.bmag[2]);
-      U.local0 = 0;
-      uint8_t* fr = frame + (size_t)f * G.fbytes;
-      const uint32_t off = xf::block_row_offset(U, gl - U.cum, 2u * q);
-      *reinterpret_cast<uint2*>(fr + off) = r0;
-      *reinterpret_cast<uint2*>(fr + off + U.pw) = r1;
-    }
   }
 }
 

@@ -35,8 +35,7 @@ __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, Frame
                                uint4*);
 __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*, const uint32_t*,
                               const uint32_t*, FrameGeom, uint32_t, uint32_t, const QTables*, uint4*, uint8_t*,
-                              unsigned long long*, uint32_t*, uint32_t);
-__global__ void k_idct_fix(const uint4*, FrameGeom, const QTables*, uint8_t*, uint32_t*, uint32_t);
+                              unsigned long long*);
 __global__ void k_huff_encode(const uint4*, const uint32_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
                               uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
@@ -192,8 +191,8 @@ struct myyuv_hip_ctx {
   DevBuf binfo; // per block: K1 -> K2's classification (binfo_word, codec_common.hpp)
   DevBuf zq;    // 256 zero bytes: K6's source for rows the mask says are zero
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
-  // K1 -> k_fdct_fix and k_decode_idct -> k_idct_fix: [0], [1] the counts of
-  // even / odd launches (fix_par), from [64] the listed units / blocks
+  // K1 -> k_fdct_fix: [0], [1] the unit counts of even / odd launches
+  // (fix_par), from [64] the units
   DevBuf fix;
   uint32_t fix_par = 0;
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
@@ -351,7 +350,7 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   // [0], [1]: overflow counts, then K2's list and (single frames) the CAP-16 tier's (launch_overflow)
   e |= c->work.grow((size_t)nblk * (nf == 1 || MYYUV_R16_BATCH ? 8 : 4) + 256);
   {
-    const size_t fb = ((size_t)nblk + 64) * 4;
+    const size_t fb = ((size_t)G.ucum[3] * nf + 64) * 4;
     if (c->fix.n < fb) {
       e |= c->fix.grow(fb);
       if (!e && (hipMemset(c->fix.p, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
@@ -512,17 +511,9 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
                  t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
   if (c->fused_dec) {  // K5 + K6 in one pass, the coefficients kept on chip
-    const uint32_t par = c->fix_par;
-    c->fix_par ^= 1u;
     e |= launch(c, MYYUV_K_HUFF_DEC, k_decode_idct, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size, cap,
                 (const StreamDesc*)desc, c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
-                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err, c->fix.as<uint32_t>(), par);
-    // the blocks whose fast-path pixels are not proven (1.6 % of the bench
-    // frame's blocks with an AC coefficient, tools/diag/fast_idct_sim.py):
-    // 64 per workgroup
-    const uint32_t grid = std::max(1u, std::min(c->fix_resident, ceil_div(nblk * nf, 64u * 16u)));
-    e |= launch(c, MYYUV_K_IDCT_FIX, k_idct_fix, dim3(grid), dim3(256), s, c->coef.as<const uint4>(), G, qt,
-                static_cast<uint8_t*>(d_out), c->fix.as<uint32_t>(), par);
+                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err);
     return e ? MYYUV_E_HIP : 0;
   }
   e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size,

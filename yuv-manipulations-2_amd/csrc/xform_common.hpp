@@ -478,101 +478,5 @@ __device__ __forceinline__ void idct_rows(float* tb, uint32_t q, const float* Qt
                                                     0x05040100u));
 }
 
-// The fused decoder's fast inverse (round 4): idct_rows with both stages as
-// FMA chains (zero steps skipped as in idct_rows), and a proof per output
-// that its pixel is the reference's.  The bound is K1's (fdct_fast) with the
-// dequantised coefficients in place of the pixels: stage 1 differs from the
-// reference's by at most 2 g8 dmax A_j per value (A_j = sum_k |Zq[k][j]|),
-// stage 2 by at most B_i = kFastBound * (S_i + dmax * A) per output of row i
-// (S_i = sum_k |U_fast[i][k]|, A = sum |Zq| over the block: integers below
-// 2^24, so its float sum is exact).  The pixel is round(clamp(R, -128, 127))
-// + 128; that map only steps at the half-integers inside the clamp range, so
-// with c = clamp(R_fast) and e = c - rint(c) the pixel is the reference's
-// whenever |e| + B_i < 0.5 (an exact tie, which roundf breaks away from zero,
-// has |e| = 0.5 and always fails).  Returns true when some output of the
-// lane fails (its block then goes to k_idct_fix, which redoes it in the
-// reference's order); the pixels are written either way.  The block's image
-// is at img (32 dwords, as idct_rows's), apart from its transpose tile tb,
-// so it is still there for the caller when the block fails.
-__device__ __forceinline__ bool idct_rows_fast(const uint32_t* img, float* tb, uint32_t q, const float* Qt,
-                                               uint2& w0, uint2& w1) {
-  uint32_t zc[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) zc[k] = img[k * 4 + q];
-  float qk[16];
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const float2 v = *reinterpret_cast<const float2*>(Qt + k * 8 + 2 * q);
-    qk[2 * k] = v.x;
-    qk[2 * k + 1] = v.y;
-  }
-  // ---- stage 1 (FMA chains) and A
-  float Um[16];  // Um[2i + h] = U[i][2q + h]
-#pragma unroll
-  for (int j = 0; j < 16; j++) Um[j] = 0.0f;
-  float a = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    if (!__any(zc[k] != 0u)) continue;
-    const float z0 = (float)(int16_t)zc[k] * qk[2 * k];
-    const float z1 = (float)(int16_t)(zc[k] >> 16) * qk[2 * k + 1];
-    a += __builtin_fabsf(z0) + __builtin_fabsf(z1);
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      Um[2 * i] = __builtin_fmaf(c_dct[k * 8 + i], z0, Um[2 * i]);
-      Um[2 * i + 1] = __builtin_fmaf(c_dct[k * 8 + i], z1, Um[2 * i + 1]);
-    }
-  }
-  a += __shfl_xor(a, 1, 64);
-  a += __shfl_xor(a, 2, 64);
-  // ---- transpose
-  float P[16];  // P[2k + h] = U[2q + h][k]
-  transpose_tile(tb, q, Um, P);
-  float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    s0 += __builtin_fabsf(P[2 * k]);
-    s1 += __builtin_fabsf(P[2 * k + 1]);
-  }
-  // the bound of both rows (the larger S_i), with margin for its own float
-  // evaluation and for the test's addition below
-  const float bnd = kFastBound * (__builtin_fmaxf(s0, s1) + 0.5f * a) * (1.0f + 0x1p-10f) + 0x1p-23f;
-  // ---- stage 2 (FMA chains): R[i][v] = sum_k U[i][k] * D[k][v]; zero columns
-  // skipped; columns v = 0..3, then 4..7 (eight sums live, not sixteen), each
-  // half rounded and packed as it is done
-  float mx = 0.0f;  // max |e| of the lane's outputs
-  uint32_t wr[4];   // w0.x, w1.x, w0.y, w1.y
-#pragma unroll
-  for (int hv = 0; hv < 2; hv++) {
-    float S[8];  // S[2(v - 4 hv) + h] = R[2q + h][v]
-#pragma unroll
-    for (int j = 0; j < 8; j++) S[j] = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      if (!__any(P[2 * k] != 0.0f || P[2 * k + 1] != 0.0f)) continue;
-#pragma unroll
-      for (int v = 0; v < 4; v++) {
-        S[2 * v] = __builtin_fmaf(P[2 * k], c_dct[k * 8 + 4 * hv + v], S[2 * v]);
-        S[2 * v + 1] = __builtin_fmaf(P[2 * k + 1], c_dct[k * 8 + 4 * hv + v], S[2 * v + 1]);
-      }
-    }
-    uint32_t px[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const float c = __builtin_amdgcn_fmed3f(S[j], -128.0f, 127.0f);
-      const float uu = c + kMagicPx;
-      mx = __builtin_fmaxf(mx, __builtin_fabsf(c - (uu - kMagicPx)));
-      px[j] = bits(uu);
-    }
-    wr[2 * hv] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[6], px[4], 0x0c0c0400u),
-                                       __builtin_amdgcn_perm(px[2], px[0], 0x0c0c0400u), 0x05040100u);
-    wr[2 * hv + 1] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[7], px[5], 0x0c0c0400u),
-                                           __builtin_amdgcn_perm(px[3], px[1], 0x0c0c0400u), 0x05040100u);
-  }
-  w0 = make_uint2(wr[0], wr[2]);
-  w1 = make_uint2(wr[1], wr[3]);
-  return mx + bnd >= 0.5f;
-}
-
 }  // namespace xf
 }  // namespace myyuv_gpu

@@ -21,7 +21,7 @@ E_BMP_INVALID, E_BMP_SIGN, E_BMP_UNSUPPORTED = 15, 16, 17
 
 KERNELS = ["fdct_quant", "huff_encode", "scan_tiles", "stream_out", "encode_tile", "huff_decode",
            "dequant_idct", "huff_encode_wide", "huff_encode_r16", "huff_encode_wave", "bmp_to_iyuv",
-           "fdct_fix", "idct_fix"]
+           "fdct_fix"]
 (K_FDCT, K_HUFF_ENC, K_SCAN, K_COMPACT, K_ENCODE_TILE, K_HUFF_DEC, K_IDCT, K_HUFF_WIDE,
  K_HUFF_R16, K_HUFF_WAVE, K_BMP) = range(11)
 
