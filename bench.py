@@ -110,11 +110,12 @@ BIG_RECOMPRESSED_SHA = "fe9b7317653c2b44a9f24436f0e349b083b4e368cf9653e8777e9f7a
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8 TB/s spec)
 SLOT_4K = 4 << 20  # batch4k payload slot: the largest of the 512 streams is 2,471,404 B (capacity is checked on device)
 # K1's VALU work (the gfx950 code object's loop body): VALU
-# instructions per lane per 16-block unit on the fast path, of which the
+# instructions per lane per 16-block unit on the fast path (with the block
+# words K1 writes for K2's classification, ~60 of them), of which the
 # transform's FMA chains (round 3's reference-order path: 660, 480); f32 VALU issue = 2 cycles per
 # wave-instruction (64 lanes on a 32-wide SIMD), 1,024 SIMDs, effective clock
 # under load from GRBM_GUI_ACTIVE (profiles/r02b_sq_counters.txt)
-K1_VALU_PER_UNIT = 488
+K1_VALU_PER_UNIT = 550
 K1_ARITH_PER_UNIT = 256
 K1_CLOCK_GHZ = 1.7
 

@@ -3,6 +3,7 @@ CPU restatement (oracle/), the reference's golden files, and — when the
 reference library built by oracle/Makefile is present — the reference itself.
 Integer/byte work: every comparison is bit-exact."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -82,6 +83,38 @@ def test_noise_vs_oracle(codec, oracle, q):
     pay = codec.compress(fr.tobytes(), w, h, q)
     assert pay == oracle.compress(fr.tobytes(), w, h, q)
     assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [(90, 90, 90), (100, 100, 100)])
+def test_fdct_unproven_units_listed_in_batches(oracle, q):
+    """K1 keeps the units its fast path cannot prove in one register per wave
+    and lists them 64 at a time (k_transform.hip).  A K1 grid of 1 % of the
+    resident workgroups (MYYUV_K1_GRID_PCT) gives each wave hundreds of units
+    of a noise batch at q90/q100, where a third to a half of them are
+    unproven, so the in-loop flush and the final one both run; every frame
+    must equal the oracle's."""
+    import myyuv_hip
+    import synth
+
+    old = os.environ.get("MYYUV_K1_GRID_PCT")
+    os.environ["MYYUV_K1_GRID_PCT"] = "1"
+    try:
+        c = myyuv_hip.Codec(0)
+    finally:
+        if old is None:
+            del os.environ["MYYUV_K1_GRID_PCT"]
+        else:
+            os.environ["MYYUV_K1_GRID_PCT"] = old
+    try:
+        w, h = 2048, 1024  # 12,288 units over ~80 waves
+        frames = [synth.noise_frame(w, h, seed=s).tobytes() for s in range(3)]
+        frames.append(blockgen.edge_frame(w, h, seed=5).tobytes())
+        got = c.compress_batch(frames, w, h, q)
+        for f, p in zip(frames, got):
+            assert p == oracle.compress(f, w, h, q)
+    finally:
+        c.close()
 
 
 @pytest.mark.parametrize("q", [(50, 50, 50), (100, 100, 100)])

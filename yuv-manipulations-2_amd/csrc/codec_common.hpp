@@ -21,6 +21,22 @@ constexpr int kSlotWords = 40;  // 160-B chunk slot per block (max chunk 155 B)
 #define MYYUV_SINK_SLOTS 1
 #endif
 constexpr uint32_t kSinkQuads = 192, kSinkSlots = MYYUV_SINK_SLOTS;
+// k_fdct_fix: waves per workgroup
+#ifndef MYYUV_FIX_WAVES
+#define MYYUV_FIX_WAVES 4
+#endif
+constexpr uint32_t kFixWaves = MYYUV_FIX_WAVES;
+// K1 -> k_fdct_fix: the unproven units in kFixLists lists (unit ua in list
+// ua % kFixLists), so their appends spread over as many atomic counters: the
+// counters of parity p (launches alternate) one per 128-B line from word 0,
+// list c from word kFixHeader at c * ceil(units / kFixLists)
+constexpr uint32_t kFixLists = 32, kFixHeader = 2 * kFixLists * 32;
+__host__ __device__ __forceinline__ uint32_t* fix_count(uint32_t* fix, uint32_t par, uint32_t c) {
+  return fix + (par * kFixLists + c) * 32u;
+}
+__host__ __device__ __forceinline__ size_t fix_words(uint32_t units) {
+  return kFixHeader + (size_t)kFixLists * ((units + kFixLists - 1) / kFixLists);
+}
 constexpr int kMaxChunk = 160;
 
 // Float-literal DCT-II basis, row u = basis u (DCT.cpp:221-230).  Literal
@@ -232,6 +248,31 @@ __host__ __device__ __forceinline__ uint32_t tile_of_block(const FrameGeom& G, u
   const uint32_t l = g - f * G.cum[3];
   const int p = l >= G.cum[1] ? (l >= G.cum[2] ? 2 : 1) : 0;
   return f * G.tcum[3] + G.tcum[p] + (l - G.cum[p]) / kK2Group;
+}
+
+// The fused decoder's non-constant blocks: transformed in the decoding wave
+// (0), or written to HBM and listed for k_idct_list (1)
+#ifndef MYYUV_DEC_AC_LIST
+#define MYYUV_DEC_AC_LIST 0
+#endif
+// The fused decoder -> k_idct_list: the non-constant blocks in kAcLists
+// lists (decode wave w appends to list w % kAcLists), counts of parity p one
+// per 128-B line, list c from word kAcHeader at c * ceil(waves / kAcLists) * 64
+constexpr uint32_t kAcLists = 32, kAcHeader = 2 * kAcLists * 32;
+__host__ __device__ __forceinline__ uint32_t* ac_count(uint32_t* l, uint32_t par, uint32_t c) {
+  return l + (par * kAcLists + c) * 32u;
+}
+__host__ __device__ __forceinline__ uint32_t* ac_list(uint32_t* l, uint32_t waves, uint32_t c) {
+  return l + kAcHeader + (size_t)c * ((waves + kAcLists - 1) / kAcLists) * 64u;
+}
+__host__ __device__ __forceinline__ size_t ac_words(uint32_t waves) {
+  return kAcHeader + (size_t)kAcLists * ((waves + kAcLists - 1) / kAcLists) * 64u;
+}
+
+// list c of K1's unproven units (see fix_count)
+__host__ __device__ __forceinline__ uint32_t* fix_list(uint32_t* fix, const FrameGeom& G, uint32_t c) {
+  const uint32_t units = G.ucum[3] * G.nframes;
+  return fix + kFixHeader + (size_t)c * ((units + kFixLists - 1) / kFixLists);
 }
 
 }  // namespace myyuv_gpu

@@ -93,6 +93,9 @@ using namespace xf;
 // K1: u8 planes -> int16 coefficients (natural order, quad layout).
 // DCT.cpp:297-306 (gather, x - 128), :269-277 (applyDCTBlock).
 typedef unsigned short k1_us2 __attribute__((ext_vector_type(2)));
+#ifndef MYYUV_K1_PKMUL
+#define MYYUV_K1_PKMUL 1
+#endif
 
 // Rows 2q, 2q+1 of lane (b, q)'s block (coefficient quads 2q, 2q+1), the
 // block's row mask (bit c: row c has a nonzero coefficient, from the block's
@@ -128,8 +131,13 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
     uint32_t fu, m16;
     asm("v_pk_min_u16 %0, %1, %2" : "=v"(fu) : "v"(wv[i]), "s"(0x00010001u));
     cnt += __builtin_bit_cast(k1_us2, fu);
+#if MYYUV_K1_PKMUL  // flag * (index + 1): the indices are VGPRs here, so the packed multiply takes them
+    asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m16) : "v"(fu), "v"(zv[i]));
+    mx = __builtin_elementwise_max(mx, __builtin_bit_cast(k1_us2, m16));
+#else
     asm("v_pk_sub_u16 %0, 0, %1" : "=v"(m16) : "v"(fu));
     mx = __builtin_elementwise_max(mx, __builtin_bit_cast(k1_us2, m16 & zv[i]));
+#endif
   }
   // the block's four lanes: counts add, msz is the maximum (one shuffle per
   // step carries both)
@@ -137,7 +145,7 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
   uint32_t msz = mx.x > mx.y ? (uint32_t)mx.x : (uint32_t)mx.y;
 #pragma unroll
   for (int d = 1; d < 4; d <<= 1) {
-    const uint32_t o = (uint32_t)__shfl_xor((int)(nnz | (msz << 16)), d, 64);
+    const uint32_t o = d == 1 ? quad_xor1(nnz | (msz << 16)) : quad_xor2(nnz | (msz << 16));
     nnz += o & 0xFFFFu;
     msz = max(msz, o >> 16);
   }
@@ -145,7 +153,7 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
   *(live ? rmask + g : reinterpret_cast<uint8_t*>(sink + 128) + lane) = (uint8_t)rm;
   // the block's four lanes store the same word (lane 4b holds row 0: the DC
   // is the low half of its lo.x)
-  const uint32_t dc = (uint32_t)__shfl((int)lo.x, (int)(lane & ~3u), 64);
+  const uint32_t dc = quad_lane0(lo.x);
   *(live ? binfo + g : reinterpret_cast<uint32_t*>(sink + 132) + lane) = binfo_word(rm, msz, class_of(nnz, msz), dc);
   *(nzl ? dlo : sink + lane) = lo;
   *(nzh ? dhi : sink + 64 + lane) = hi;
@@ -158,10 +166,15 @@ __device__ __forceinline__ void stage_zz(uint4* szz) {
 }
 
 // K1's exact path out of line (MYYUV_K1_INLINE_EXACT 0): a unit whose fast
-// result is not provably the reference's is listed in fix (fix[par] the
-// count, fix[64 + i] the batch unit; par alternates from launch to launch) by
-// K1 and transformed by k_fdct_fix, which runs next in the stream.  Kept in K1, the exact path's code raised K1 from 64 to
-// 99 VGPRs (7 -> 5 waves per SIMD) and cost it 15 % (profiles/r4g_*).
+// result is not provably the reference's is appended by K1 to one of
+// kFixLists lists (unit ua to list ua % kFixLists, fix_count / fix_list in
+// codec_common.hpp; each launch uses the counts of its parity `par`) and
+// transformed by k_fdct_fix, which runs next in the stream.  Kept in K1, the
+// exact path's code raised K1 from 64 to 99 VGPRs (7 -> 5 waves per SIMD) and
+// cost it 15 % (profiles/r4g_*).  One count for all units serialised the
+// appends on one address (at q90, 18 % of the units: 47k atomics per
+// 8192x8192 frame, K1 83 -> 215 us); a per-wave register list flushed 64 at a
+// time fixed that but cost K1 4 % at q50 (profiles/r4r_*).
 #ifndef MYYUV_K1_INLINE_EXACT
 #define MYYUV_K1_INLINE_EXACT 0
 #endif
@@ -243,34 +256,49 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
 #else
     uint32_t xr[4];
     fdct_load(img, q, xr);
-    if (!fdct_fast(xr, tb, q, sqr, U.p, store) && lane == 0) fix[64 + atomicAdd(fix + par, 1u)] = ua;
+    if (!fdct_fast(xr, tb, q, sqr, U.p, store) && lane == 0) {
+      const uint32_t c = ua % kFixLists;
+      fix_list(fix, G, c)[atomicAdd(fix_count(fix, par, c), 1u)] = ua;
+    }
 #endif
   }
 }
 
-// K1's exact path for the units K1 listed (fix[par] of them at fix + 64): a
-// wave per listed unit, the reference's order (fdct_exact), the same stores.
-// Workgroup 0 zeroes the other parity's count, which the next K1 fills (the
-// previous fix launch, its reader, is done: stream order).
-__global__ __launch_bounds__(256) void k_fdct_fix(const uint8_t* __restrict__ frame, FrameGeom G,
+// K1's exact path for the units K1 listed (kFixLists lists, the counts of
+// parity par): a wave per listed unit, the reference's order (fdct_exact),
+// the same stores.  Wave w takes list w % kFixLists (the grid's waves are a
+// multiple of kFixLists).  Workgroup 0 zeroes the other parity's counts, which
+// the next K1 fills (the previous fix launch, their reader, is done: stream
+// order).
+__global__ __launch_bounds__(64 * kFixWaves) void k_fdct_fix(const uint8_t* __restrict__ frame, FrameGeom G,
                                                   const QTables* __restrict__ qt, uint4* __restrict__ coef,
                                                   uint8_t* __restrict__ rmask, uint32_t* __restrict__ binfo,
                                                   uint4* __restrict__ sink,
                                                   uint32_t* __restrict__ fix, uint32_t par) {
-  __shared__ float tile[4][kXfUnit * kTile];
+  __shared__ float tile[kFixWaves][kXfUnit * kTile];
   __shared__ float sqr[2 * 3 * 64];
   __shared__ uint4 szz[8];
-  if (blockIdx.x == 0 && threadIdx.x == 0) fix[par ^ 1u] = 0u;
-  const uint32_t n = __builtin_amdgcn_readfirstlane(fix[par]);
-  if (blockIdx.x * 4u >= n) return;  // (uniform over the workgroup)
+  __shared__ uint32_t s_any;
+  if (blockIdx.x == 0 && threadIdx.x < kFixLists) *fix_count(fix, par ^ 1u, threadIdx.x) = 0u;
+  if (threadIdx.x == 0) s_any = 0u;
+  __syncthreads();
+  const uint32_t gw = blockIdx.x * kFixWaves + (threadIdx.x >> 6), nw = gridDim.x * kFixWaves;
+  const uint32_t c = gw % kFixLists;
+  const uint32_t n = __builtin_amdgcn_readfirstlane(*fix_count(fix, par, c));
+  if ((threadIdx.x & 63u) == 0 && gw / kFixLists < n) s_any = 1u;
+  __syncthreads();
+  if (s_any == 0u) return;  // (uniform over the workgroup)
   stage_zz(szz);
-  stage_tables<2 * 3 * 64>(qt->q[0], sqr);
+#pragma unroll
+  for (uint32_t i = threadIdx.x; i < 2u * 3u * 64u; i += 64u * kFixWaves) sqr[i] = qt->q[0][i];
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t q = lane & 3u, b = lane >> 2;
   float* tb = tile[threadIdx.x >> 6] + b * kTile;
   uint8_t* img = reinterpret_cast<uint8_t*>(tb);
-  for (uint32_t i = first_unit(); i < n; i += unit_stride()) {
-    const uint32_t ua = __builtin_amdgcn_readfirstlane(fix[64 + i]);
+  const uint32_t* list = fix_list(fix, G, c);
+  for (uint32_t i = gw / kFixLists; i < n; i += nw / kFixLists) {
+    const uint32_t ua = __builtin_amdgcn_readfirstlane(list[i]);
     const uint32_t f = div_magic(ua, G.umag);
     const Unit U = unit_of(G, ua - f * G.ucum[3]);
     const uint32_t local = U.local0 + b;
@@ -289,6 +317,61 @@ __global__ __launch_bounds__(256) void k_fdct_fix(const uint8_t* __restrict__ fr
                [&](const uint32_t (&c)[16]) {
                  store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
                });
+  }
+}
+
+// The fused decoder's non-constant blocks (MYYUV_DEC_AC_LIST): their
+// coefficients in K5's layout (nonzero rows, row masks), listed in kAcLists
+// lists (ac_count / ac_list, parity par; dwaves: the decoder's waves) ->
+// pixels.  K6's body on units of 16 listed blocks (any frames and planes: each
+// lane's block has its own plane and position); wave w takes list w %
+// kAcLists.  Workgroup 0 zeroes the other parity's counts for the next
+// decoder launch (stream order).
+__global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_idct_list(const uint4* __restrict__ coef,
+                                                  const uint8_t* __restrict__ rmask,
+                                                  const uint4* __restrict__ zq, FrameGeom G,
+                                                  const QTables* __restrict__ qt, uint8_t* __restrict__ frame,
+                                                  uint4* __restrict__ sink, uint32_t* __restrict__ aclist,
+                                                  uint32_t par, uint32_t dwaves) {
+  __shared__ float tile[4][kXfUnit * kTile];
+  __shared__ float sq[3 * 64];  // QTables::q
+  if (blockIdx.x == 0 && threadIdx.x < kAcLists) *ac_count(aclist, par ^ 1u, threadIdx.x) = 0u;
+  stage_tables<3 * 64>(qt->q[0], sq);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t q = lane & 3u, b = lane >> 2;
+  float* tb = tile[threadIdx.x >> 6] + b * kTile;
+  uint32_t* tw = reinterpret_cast<uint32_t*>(tb);
+  const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6)), nw = gridDim.x * 4u;
+  const uint32_t c = gw % kAcLists;
+  const uint32_t n = __builtin_amdgcn_readfirstlane(*ac_count(aclist, par, c));
+  const uint32_t* list = ac_list(aclist, dwaves, c);
+  const uint32_t cum3 = G.cum[3];
+  for (uint32_t e0 = 16u * (gw / kAcLists); e0 < n; e0 += 16u * (nw / kAcLists)) {
+    const bool live = e0 + b < n;
+    const uint32_t g = list[live ? e0 + b : e0];
+    uint4 a, cq;
+    load_quads(coef, zq, g, q, rmask[g], a, cq);
+    wave_sync();  // (the previous unit's tile reads are done)
+    *reinterpret_cast<uint4*>(tw + 8 * q) = a;
+    *reinterpret_cast<uint4*>(tw + 8 * q + 4) = cq;
+    wave_sync();
+    const uint32_t f = g / cum3, gl = g - f * cum3;
+    const bool p1 = gl >= G.cum[1], p2 = gl >= G.cum[2];
+    uint2 w0, w1;
+    idct_rows(tb, q, sq + (p2 ? 128 : (p1 ? 64 : 0)), w0, w1);
+    Unit U;
+    U.p = p2 ? 2 : (p1 ? 1 : 0);
+    U.cum = pick(p1, p2, G.cum[0], G.cum[1], G.cum[2]);
+    U.poff = pick(p1, p2, G.poff[0], G.poff[1], G.poff[2]);
+    U.pw = pick(p1, p2, G.pw[0], G.pw[1], G.pw[2]);
+    U.bw = pick(p1, p2, G.bw[0], G.bw[1], G.bw[2]);
+    U.bmag = pick(p1, p2, G.bmag[0], G.bmag[1], G.bmag[2]);
+    U.local0 = 0;
+    U.nb = 0;
+    const uint32_t off = block_row_offset(U, gl - U.cum, 2u * q);
+    uint8_t* fr = frame + (size_t)f * G.fbytes;
+    *(live ? reinterpret_cast<uint2*>(fr + off) : reinterpret_cast<uint2*>(sink + lane)) = w0;
+    *(live ? reinterpret_cast<uint2*>(fr + off + U.pw) : reinterpret_cast<uint2*>(sink + 64 + lane)) = w1;
   }
 }
 

@@ -35,7 +35,9 @@ __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, Frame
                                uint4*);
 __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*, const uint32_t*,
                               const uint32_t*, FrameGeom, uint32_t, uint32_t, const QTables*, uint4*, uint8_t*,
-                              unsigned long long*);
+                              unsigned long long*, uint8_t*, uint32_t*, uint32_t);
+__global__ void k_idct_list(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*, uint4*,
+                            uint32_t*, uint32_t, uint32_t);
 __global__ void k_huff_encode(const uint4*, const uint32_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
                               uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
@@ -191,10 +193,14 @@ struct myyuv_hip_ctx {
   DevBuf binfo; // per block: K1 -> K2's classification (binfo_word, codec_common.hpp)
   DevBuf zq;    // 256 zero bytes: K6's source for rows the mask says are zero
   DevBuf sink;  // K1/K6 stores of lanes past a plane's end (128 x 16 B, never read)
-  // K1 -> k_fdct_fix: [0], [1] the unit counts of even / odd launches
-  // (fix_par), from [64] the units
+  // K1 -> k_fdct_fix: the unproven units' lists and counts (fix_count /
+  // fix_list, codec_common.hpp; fix_par alternates from launch to launch)
   DevBuf fix;
   uint32_t fix_par = 0;
+  // fused decoder -> k_idct_list (MYYUV_DEC_AC_LIST): the non-constant blocks'
+  // lists and counts (ac_count / ac_list), parity alternating per launch
+  DevBuf aclist;
+  uint32_t ac_par = 0;
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
   uint32_t fix_resident = kXfWaves / 4;                      // k_fdct_fix workgroups resident
   uint32_t fix_grid = 64;  // k_fdct_fix's grid at qualities up to fix_qmax (MYYUV_FIX_GRID, 0: resident)
@@ -350,10 +356,18 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   // [0], [1]: overflow counts, then K2's list and (single frames) the CAP-16 tier's (launch_overflow)
   e |= c->work.grow((size_t)nblk * (nf == 1 || MYYUV_R16_BATCH ? 8 : 4) + 256);
   {
-    const size_t fb = ((size_t)G.ucum[3] * nf + 64) * 4;
+    const size_t fb = fix_words(G.ucum[3] * nf) * 4;
     if (c->fix.n < fb) {
       e |= c->fix.grow(fb);
-      if (!e && (hipMemset(c->fix.p, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+      if (!e && (hipMemset(c->fix.p, 0, kFixHeader * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+        e |= MYYUV_E_HIP;
+    }
+  }
+  if (MYYUV_DEC_AC_LIST) {
+    const size_t ab = ac_words(nwaves + 3 * nf) * 4;  // (the decoder's waves: per plane, rounded up)
+    if (c->aclist.n < ab) {
+      e |= c->aclist.grow(ab);
+      if (!e && (hipMemset(c->aclist.p, 0, kAcHeader * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
         e |= MYYUV_E_HIP;
     }
   }
@@ -451,8 +465,10 @@ int launch_fdct(myyuv_hip_ctx* c, const FrameGeom& G, const uint8_t* in, const Q
   for (int p = 0; p < 3; p++) qmax = std::max(qmax, (uint32_t)c->q_cached[p]);
   const uint32_t want =
       (c->fix_grid == 0 || !c->q_valid || qmax > c->fix_qmax) ? c->fix_resident : c->fix_grid;
-  const uint32_t grid = std::max(1u, std::min(want, ceil_div(G.ucum[3] * G.nframes, 4)));
-  e |= launch(c, MYYUV_K_FDCT_FIX, k_fdct_fix, dim3(grid), dim3(256), s, in, G, qt, c->coef.as<uint4>(),
+  // (a multiple of kFixLists waves: wave w takes list w % kFixLists)
+  const uint32_t per = kFixLists / kFixWaves;
+  const uint32_t grid = std::max(per, (want * 4 / kFixWaves) / per * per);
+  e |= launch(c, MYYUV_K_FDCT_FIX, k_fdct_fix, dim3(grid), dim3(64 * kFixWaves), s, in, G, qt, c->coef.as<uint4>(),
               c->rmask.as<uint8_t>(), c->binfo.as<uint32_t>(), c->sink.as<uint4>(), c->fix.as<uint32_t>(), par);
   return e;
 }
@@ -511,9 +527,19 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
                  t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
   if (c->fused_dec) {  // K5 + K6 in one pass, the coefficients kept on chip
+    const uint32_t par = c->ac_par;
+    c->ac_par ^= 1u;
     e |= launch(c, MYYUV_K_HUFF_DEC, k_decode_idct, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size, cap,
                 (const StreamDesc*)desc, c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
-                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err);
+                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err, c->rmask.as<uint8_t>(),
+                c->aclist.as<uint32_t>(), par);
+    if (MYYUV_DEC_AC_LIST) {  // the non-constant blocks' transform, at K6's occupancy
+      const uint32_t per = kAcLists / 4;
+      const uint32_t grid = std::max(per, c->xf_resident[0] / per * per);
+      e |= launch(c, MYYUV_K_IDCT, k_idct_list, dim3(grid), dim3(256), s, c->coef.as<const uint4>(),
+                  c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G, qt, static_cast<uint8_t*>(d_out),
+                  c->sink.as<uint4>(), c->aclist.as<uint32_t>(), par, (t0 + t1 + t2) * nf);
+    }
     return e ? MYYUV_E_HIP : 0;
   }
   e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size,
@@ -650,8 +676,9 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
       c->xf_resident[0] = (uint32_t)(cus * n1);
       c->xf_resident[1] = (uint32_t)(cus * n6);
       int nfix = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nfix, k_fdct_fix, 256, 0) == hipSuccess && nfix > 0)
-        c->fix_resident = (uint32_t)(cus * nfix);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nfix, k_fdct_fix, 64 * kFixWaves, 0) == hipSuccess &&
+          nfix > 0)
+        c->fix_resident = (uint32_t)(cus * nfix) * kFixWaves / 4;  // (in 4-wave workgroups)
       if (const char* v = std::getenv("MYYUV_FIX_GRID")) c->fix_grid = (uint32_t)std::atoi(v);
       if (const char* v = std::getenv("MYYUV_FIX_QMAX")) c->fix_qmax = (uint32_t)std::atoi(v);
       {
@@ -690,7 +717,7 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   (void)hipEventDestroy(c->done);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->stage, &c->oslots, &c->tinfo, &c->srcoff, &c->sizes, &c->loff, &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
-                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes, &c->fix, &c->binfo};
+                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes, &c->fix, &c->binfo, &c->aclist};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;

@@ -34,6 +34,39 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Exchanges inside a block's four lanes (a DPP quad: lanes 4b .. 4b+3).  The
+// callers run with the whole wave active (K1's loop, k_fdct_fix's, the fused
+// encoder's phase 1: every branch around them is wave-uniform), so every
+// source lane is active; MYYUV_QUAD_DPP 0 uses ds_bpermute instead.
+#ifndef MYYUV_QUAD_DPP
+#define MYYUV_QUAD_DPP 1
+#endif
+template <int kCtrl>  // quad_perm control
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kCtrl, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t quad_xor1(uint32_t v) {
+#if MYYUV_QUAD_DPP
+  return quad_perm<0xB1>(v);  // [1, 0, 3, 2]
+#else
+  return (uint32_t)__shfl_xor((int)v, 1, 64);
+#endif
+}
+__device__ __forceinline__ uint32_t quad_xor2(uint32_t v) {
+#if MYYUV_QUAD_DPP
+  return quad_perm<0x4E>(v);  // [2, 3, 0, 1]
+#else
+  return (uint32_t)__shfl_xor((int)v, 2, 64);
+#endif
+}
+__device__ __forceinline__ uint32_t quad_lane0(uint32_t v) {
+#if MYYUV_QUAD_DPP
+  return quad_perm<0x00>(v);  // [0, 0, 0, 0]
+#else
+  return (uint32_t)__shfl((int)v, (int)((threadIdx.x & 63u) & ~3u), 64);
+#endif
+}
+
 // Keeps 16 accumulators' updates in round-robin order (the scheduler would
 // otherwise serialise them chain by chain to save registers).
 __device__ __forceinline__ void fence16(float (&a)[16]) {
@@ -280,8 +313,8 @@ __device__ __forceinline__ bool fdct_fast(const uint32_t (&xr)[4], float* tb, ui
   uint32_t a = 0;
 #pragma unroll
   for (int m = 0; m < 4; m++) a = __builtin_amdgcn_sad_u8(xr[m] ^ 0x80808080u, 0x80808080u, a);
-  a += (uint32_t)__shfl_xor((int)a, 1, 64);
-  a += (uint32_t)__shfl_xor((int)a, 2, 64);
+  a += quad_xor1(a);
+  a += quad_xor2(a);
   // ---- stage 1 (fast), transpose: columns (2q, 2q+1) in, rows (2q, 2q+1) out
   float T[16];
   fdct_stage1<true>(xr, T);
@@ -368,7 +401,7 @@ __device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_
                                           Emit&& emit) {
   uint32_t xr[4];
   fdct_load(img, q, xr);
-  if (!fdct_fast(xr, tb, q, sqr, p, emit)) {
+  if (__builtin_expect(!fdct_fast(xr, tb, q, sqr, p, emit), 0)) {
     wave_sync();
     fdct_exact(xr, tb, q, sqr, p, emit);
   }
@@ -389,8 +422,8 @@ __device__ __forceinline__ void pack_quads(const uint32_t (&c)[16], uint32_t q, 
   hi.w = __builtin_amdgcn_perm(c[15], c[13], 0x05040100u);
   const bool nzl = (lo.x | lo.y | lo.z | lo.w) != 0u, nzh = (hi.x | hi.y | hi.z | hi.w) != 0u;
   rm = (nzl ? 1u << (2 * q) : 0u) | (nzh ? 2u << (2 * q) : 0u);
-  rm |= __shfl_xor(rm, 1, 64);
-  rm |= __shfl_xor(rm, 2, 64);
+  rm |= quad_xor1(rm);
+  rm |= quad_xor2(rm);
 }
 
 // K6's body for lane (b, q) of a 16-block unit (DCT.cpp:325-335, :358-362):
@@ -476,6 +509,78 @@ __device__ __forceinline__ void idct_rows(float* tb, uint32_t q, const float* Qt
                               __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[15], px[13], 0x0c0c0400u),
                                                     __builtin_amdgcn_perm(px[11], px[9], 0x0c0c0400u),
                                                     0x05040100u));
+}
+
+// idct_rows with a smaller register peak, for the fused decoder, where every
+// lane's 32 coefficient words stay live through the unit loop: the same
+// products and sums in the same order (so the same pixels), but each
+// coefficient word and Q pair loaded at its step, and stage 2 in two halves
+// of four output columns (eight sums live, not sixteen).
+__device__ __forceinline__ void fence8(float (&a)[8]) {
+  asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
+               "+v"(a[7]));
+}
+__device__ __forceinline__ void idct_rows_lean(float* tb, uint32_t q, const float* Qt, uint2& w0, uint2& w1) {
+  const uint32_t* tw = reinterpret_cast<const uint32_t*>(tb);
+  // ---- dequantise and stage 1 (DCT.cpp:331, 256-266), zero rows skipped
+  float Um[16];  // Um[2i + h] = U[i][2q + h]
+#pragma unroll
+  for (int j = 0; j < 16; j++) Um[j] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t zk = tw[k * 4 + q];
+    if (!__any(zk != 0u)) continue;
+    const float2 qv = *reinterpret_cast<const float2*>(Qt + k * 8 + 2 * q);
+    const float z0 = (float)(int16_t)zk * qv.x;
+    const float z1 = (float)(int16_t)(zk >> 16) * qv.y;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      Um[2 * i] = Um[2 * i] + c_dct[k * 8 + i] * z0;
+      Um[2 * i + 1] = Um[2 * i + 1] + c_dct[k * 8 + i] * z1;
+    }
+    fence16(Um);
+  }
+  wave_sync();  // (the image is read; the transpose rewrites the tile)
+  float P[16];  // P[2k + h] = U[2q + h][k]
+  transpose_tile(tb, q, Um, P);
+  // ---- stage 2 (squareMatrixMul<8>(U, DCT)), columns 0..3 then 4..7, zero
+  // columns skipped; clamp(roundf(R) + 128) (DCT.cpp:358-362) per half
+  uint32_t wr[4];  // w0.x, w1.x, w0.y, w1.y
+#pragma unroll
+  for (int hv = 0; hv < 2; hv++) {
+    float S[8];  // S[2(v - 4 hv) + h] = R[2q + h][v]
+#pragma unroll
+    for (int j = 0; j < 8; j++) S[j] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (!__any(P[2 * k] != 0.0f || P[2 * k + 1] != 0.0f)) continue;
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        S[2 * v] = S[2 * v] + P[2 * k] * c_dct[k * 8 + 4 * hv + v];
+        S[2 * v + 1] = S[2 * v + 1] + P[2 * k + 1] * c_dct[k * 8 + 4 * hv + v];
+      }
+      fence8(S);
+    }
+    uint32_t px[8];
+    bool tie = false;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      S[j] = __builtin_amdgcn_fmed3f(S[j], -128.0f, 127.0f);
+      tie = tie || __builtin_amdgcn_fractf(S[j]) == 0.5f;
+      px[j] = bits(S[j] + kMagicPx);
+    }
+    if (tie) {
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        px[j] = (uint32_t)((int)__builtin_truncf(S[j] + __builtin_copysignf(kHalfDown, S[j])) + 128);
+    }
+    wr[2 * hv] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[6], px[4], 0x0c0c0400u),
+                                       __builtin_amdgcn_perm(px[2], px[0], 0x0c0c0400u), 0x05040100u);
+    wr[2 * hv + 1] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[7], px[5], 0x0c0c0400u),
+                                           __builtin_amdgcn_perm(px[3], px[1], 0x0c0c0400u), 0x05040100u);
+  }
+  w0 = make_uint2(wr[0], wr[2]);
+  w1 = make_uint2(wr[1], wr[3]);
 }
 
 }  // namespace xf
