@@ -250,25 +250,6 @@ __host__ __device__ __forceinline__ uint32_t tile_of_block(const FrameGeom& G, u
   return f * G.tcum[3] + G.tcum[p] + (l - G.cum[p]) / kK2Group;
 }
 
-// The fused decoder's non-constant blocks: transformed in the decoding wave
-// (0), or written to HBM and listed for k_idct_list (1)
-#ifndef MYYUV_DEC_AC_LIST
-#define MYYUV_DEC_AC_LIST 0
-#endif
-// The fused decoder -> k_idct_list: the non-constant blocks in kAcLists
-// lists (decode wave w appends to list w % kAcLists), counts of parity p one
-// per 128-B line, list c from word kAcHeader at c * ceil(waves / kAcLists) * 64
-constexpr uint32_t kAcLists = 32, kAcHeader = 2 * kAcLists * 32;
-__host__ __device__ __forceinline__ uint32_t* ac_count(uint32_t* l, uint32_t par, uint32_t c) {
-  return l + (par * kAcLists + c) * 32u;
-}
-__host__ __device__ __forceinline__ uint32_t* ac_list(uint32_t* l, uint32_t waves, uint32_t c) {
-  return l + kAcHeader + (size_t)c * ((waves + kAcLists - 1) / kAcLists) * 64u;
-}
-__host__ __device__ __forceinline__ size_t ac_words(uint32_t waves) {
-  return kAcHeader + (size_t)kAcLists * ((waves + kAcLists - 1) / kAcLists) * 64u;
-}
-
 // list c of K1's unproven units (see fix_count)
 __host__ __device__ __forceinline__ uint32_t* fix_list(uint32_t* fix, const FrameGeom& G, uint32_t c) {
   const uint32_t units = G.ucum[3] * G.nframes;

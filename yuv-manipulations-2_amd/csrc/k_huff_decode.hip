@@ -49,12 +49,6 @@ constexpr uint32_t kStageQuads = 384;
 // the value needs no select.
 constexpr uint32_t kZeroBit = kStageQuads * 128u;
 
-// the fused decoder's transform: idct_rows_lean (1: a smaller register peak,
-// the same arithmetic) or idct_rows (0)
-#ifndef MYYUV_DEC_LEAN
-#define MYYUV_DEC_LEAN 0
-#endif
-
 // diagnostic ablations (never the product; 4: the non-constant blocks'
 // transform replaced by a copy, stores kept): 1 = no symbol decode, 2 = no
 // table parse either, 3 = the fused decoder skips its transform
@@ -504,9 +498,7 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
                                                    uint32_t tiles_p1, const QTables* __restrict__ qt,
                                                    uint4* __restrict__ coef,
                                                    uint8_t* __restrict__ frame,
-                                                   unsigned long long* __restrict__ err,
-                                                   uint8_t* __restrict__ rmask, uint32_t* __restrict__ aclist,
-                                                   uint32_t par) {
+                                                   unsigned long long* __restrict__ err) {
   static_assert(sizeof(uint4) * kStageQuads >= sizeof(float) * xf::kXfTile16, "the tile over the stage");
   __shared__ uint4 stq[kStageQuads + 1];
   __shared__ float sq[64];
@@ -587,38 +579,6 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
       *reinterpret_cast<uint2*>(fr + off) = row;
     }
   }
-#if MYYUV_DEC_AC_LIST
-  // the other blocks: nonzero coefficient rows and row mask to HBM (K5's
-  // layout), the block listed for k_idct_list (list wave % kAcLists, one
-  // atomic per wave)
-  {
-    const bool ac = D.live && !isdc;
-    if (ac) {
-      const uint32_t gg = D.gbase + D.g;
-      uint32_t m = 0xFFu;
-      if (!direct) {
-        m = 0;
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-          const bool nz = (nw[4 * c] | nw[4 * c + 1] | nw[4 * c + 2] | nw[4 * c + 3]) != 0u;
-          m |= nz ? 1u << c : 0u;
-          if (nz) coef[coef_quad(gg, c)] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
-        }
-      }
-      rmask[gg] = (uint8_t)m;
-    }
-    const uint64_t am = __ballot(ac);
-    if (am) {
-      const uint32_t wid = blockIdx.y * gridDim.x + blockIdx.x, c = wid % kAcLists;
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(ac_count(aclist, par, c), (uint32_t)__popcll(am));
-      base = __builtin_amdgcn_readfirstlane(base);
-      if (ac) ac_list(aclist, gridDim.x * gridDim.y, c)[base + (uint32_t)__popcll(am & ((1ull << lane) - 1ull))] =
-          D.gbase + D.g;
-    }
-  }
-  return;
-#endif
   // (compacted in block order: ordering the units by sparsity kind — row 0
   // only, column 0 only, the rest — measured no faster, profiles/r3zl_*)
   const uint64_t rest = __ballot(D.live && !isdc);
@@ -652,8 +612,6 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
       w0 = make_uint2(tw[q], tw[4 + q]);
       w1 = make_uint2(tw[8 + q], tw[12 + q]);
     }
-#elif MYYUV_DEC_LEAN
-    xf::idct_rows_lean(tile + b * xf::kTile, q, sq, w0, w1);
 #else
     xf::idct_rows(tile + b * xf::kTile, q, sq, w0, w1);
 #endif

@@ -178,6 +178,9 @@ __device__ __forceinline__ void stage_zz(uint4* szz) {
 #ifndef MYYUV_K1_INLINE_EXACT
 #define MYYUV_K1_INLINE_EXACT 0
 #endif
+#ifndef MYYUV_FIX_SPREAD
+#define MYYUV_FIX_SPREAD 1  // (0, A/B builds only: every unit in list 0)
+#endif
 
 __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t* __restrict__ frame, FrameGeom G,
                                                    const QTables* __restrict__ qt,
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
     uint32_t xr[4];
     fdct_load(img, q, xr);
     if (!fdct_fast(xr, tb, q, sqr, U.p, store) && lane == 0) {
-      const uint32_t c = ua % kFixLists;
+      const uint32_t c = MYYUV_FIX_SPREAD ? ua % kFixLists : 0u;
       fix_list(fix, G, c)[atomicAdd(fix_count(fix, par, c), 1u)] = ua;
     }
 #endif
@@ -317,61 +320,6 @@ __global__ __launch_bounds__(64 * kFixWaves) void k_fdct_fix(const uint8_t* __re
                [&](const uint32_t (&c)[16]) {
                  store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
                });
-  }
-}
-
-// The fused decoder's non-constant blocks (MYYUV_DEC_AC_LIST): their
-// coefficients in K5's layout (nonzero rows, row masks), listed in kAcLists
-// lists (ac_count / ac_list, parity par; dwaves: the decoder's waves) ->
-// pixels.  K6's body on units of 16 listed blocks (any frames and planes: each
-// lane's block has its own plane and position); wave w takes list w %
-// kAcLists.  Workgroup 0 zeroes the other parity's counts for the next
-// decoder launch (stream order).
-__global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_idct_list(const uint4* __restrict__ coef,
-                                                  const uint8_t* __restrict__ rmask,
-                                                  const uint4* __restrict__ zq, FrameGeom G,
-                                                  const QTables* __restrict__ qt, uint8_t* __restrict__ frame,
-                                                  uint4* __restrict__ sink, uint32_t* __restrict__ aclist,
-                                                  uint32_t par, uint32_t dwaves) {
-  __shared__ float tile[4][kXfUnit * kTile];
-  __shared__ float sq[3 * 64];  // QTables::q
-  if (blockIdx.x == 0 && threadIdx.x < kAcLists) *ac_count(aclist, par ^ 1u, threadIdx.x) = 0u;
-  stage_tables<3 * 64>(qt->q[0], sq);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t q = lane & 3u, b = lane >> 2;
-  float* tb = tile[threadIdx.x >> 6] + b * kTile;
-  uint32_t* tw = reinterpret_cast<uint32_t*>(tb);
-  const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6)), nw = gridDim.x * 4u;
-  const uint32_t c = gw % kAcLists;
-  const uint32_t n = __builtin_amdgcn_readfirstlane(*ac_count(aclist, par, c));
-  const uint32_t* list = ac_list(aclist, dwaves, c);
-  const uint32_t cum3 = G.cum[3];
-  for (uint32_t e0 = 16u * (gw / kAcLists); e0 < n; e0 += 16u * (nw / kAcLists)) {
-    const bool live = e0 + b < n;
-    const uint32_t g = list[live ? e0 + b : e0];
-    uint4 a, cq;
-    load_quads(coef, zq, g, q, rmask[g], a, cq);
-    wave_sync();  // (the previous unit's tile reads are done)
-    *reinterpret_cast<uint4*>(tw + 8 * q) = a;
-    *reinterpret_cast<uint4*>(tw + 8 * q + 4) = cq;
-    wave_sync();
-    const uint32_t f = g / cum3, gl = g - f * cum3;
-    const bool p1 = gl >= G.cum[1], p2 = gl >= G.cum[2];
-    uint2 w0, w1;
-    idct_rows(tb, q, sq + (p2 ? 128 : (p1 ? 64 : 0)), w0, w1);
-    Unit U;
-    U.p = p2 ? 2 : (p1 ? 1 : 0);
-    U.cum = pick(p1, p2, G.cum[0], G.cum[1], G.cum[2]);
-    U.poff = pick(p1, p2, G.poff[0], G.poff[1], G.poff[2]);
-    U.pw = pick(p1, p2, G.pw[0], G.pw[1], G.pw[2]);
-    U.bw = pick(p1, p2, G.bw[0], G.bw[1], G.bw[2]);
-    U.bmag = pick(p1, p2, G.bmag[0], G.bmag[1], G.bmag[2]);
-    U.local0 = 0;
-    U.nb = 0;
-    const uint32_t off = block_row_offset(U, gl - U.cum, 2u * q);
-    uint8_t* fr = frame + (size_t)f * G.fbytes;
-    *(live ? reinterpret_cast<uint2*>(fr + off) : reinterpret_cast<uint2*>(sink + lane)) = w0;
-    *(live ? reinterpret_cast<uint2*>(fr + off + U.pw) : reinterpret_cast<uint2*>(sink + 64 + lane)) = w1;
   }
 }
 

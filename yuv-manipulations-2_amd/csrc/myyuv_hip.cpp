@@ -35,9 +35,7 @@ __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, Frame
                                uint4*);
 __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*, const uint32_t*,
                               const uint32_t*, FrameGeom, uint32_t, uint32_t, const QTables*, uint4*, uint8_t*,
-                              unsigned long long*, uint8_t*, uint32_t*, uint32_t);
-__global__ void k_idct_list(const uint4*, const uint8_t*, const uint4*, FrameGeom, const QTables*, uint8_t*, uint4*,
-                            uint32_t*, uint32_t, uint32_t);
+                              unsigned long long*);
 __global__ void k_huff_encode(const uint4*, const uint32_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
                               uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
@@ -197,10 +195,6 @@ struct myyuv_hip_ctx {
   // fix_list, codec_common.hpp; fix_par alternates from launch to launch)
   DevBuf fix;
   uint32_t fix_par = 0;
-  // fused decoder -> k_idct_list (MYYUV_DEC_AC_LIST): the non-constant blocks'
-  // lists and counts (ac_count / ac_list), parity alternating per launch
-  DevBuf aclist;
-  uint32_t ac_par = 0;
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
   uint32_t fix_resident = kXfWaves / 4;                      // k_fdct_fix workgroups resident
   uint32_t fix_grid = 64;  // k_fdct_fix's grid at qualities up to fix_qmax (MYYUV_FIX_GRID, 0: resident)
@@ -363,14 +357,6 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
         e |= MYYUV_E_HIP;
     }
   }
-  if (MYYUV_DEC_AC_LIST) {
-    const size_t ab = ac_words(nwaves + 3 * nf) * 4;  // (the decoder's waves: per plane, rounded up)
-    if (c->aclist.n < ab) {
-      e |= c->aclist.grow(ab);
-      if (!e && (hipMemset(c->aclist.p, 0, kAcHeader * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
-        e |= MYYUV_E_HIP;
-    }
-  }
   const size_t st_bytes = (size_t)nf * (ntiles + 1) * 8;
   if (c->status.n < st_bytes) {
     e |= c->status.grow(st_bytes);
@@ -527,19 +513,9 @@ int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
                  t1 = ceil_div(G.cum[2] - G.cum[1], kWave),
                  t2 = ceil_div(G.cum[3] - G.cum[2], kWave);
   if (c->fused_dec) {  // K5 + K6 in one pass, the coefficients kept on chip
-    const uint32_t par = c->ac_par;
-    c->ac_par ^= 1u;
     e |= launch(c, MYYUV_K_HUFF_DEC, k_decode_idct, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size, cap,
                 (const StreamDesc*)desc, c->loff.as<const uint32_t>(), c->tiles.as<const uint32_t>(), G, t0, t1,
-                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err, c->rmask.as<uint8_t>(),
-                c->aclist.as<uint32_t>(), par);
-    if (MYYUV_DEC_AC_LIST) {  // the non-constant blocks' transform, at K6's occupancy
-      const uint32_t per = kAcLists / 4;
-      const uint32_t grid = std::max(per, c->xf_resident[0] / per * per);
-      e |= launch(c, MYYUV_K_IDCT, k_idct_list, dim3(grid), dim3(256), s, c->coef.as<const uint4>(),
-                  c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G, qt, static_cast<uint8_t*>(d_out),
-                  c->sink.as<uint4>(), c->aclist.as<uint32_t>(), par, (t0 + t1 + t2) * nf);
-    }
+                qt, c->coef.as<uint4>(), static_cast<uint8_t*>(d_out), err);
     return e ? MYYUV_E_HIP : 0;
   }
   e |= launch(c, MYYUV_K_HUFF_DEC, k_huff_decode, dim3(t0 + t1 + t2, nf), dim3(kWave), s, in, d_size,
@@ -717,7 +693,7 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   (void)hipEventDestroy(c->done);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->stage, &c->oslots, &c->tinfo, &c->srcoff, &c->sizes, &c->loff, &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
-                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes, &c->fix, &c->binfo, &c->aclist};
+                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes, &c->fix, &c->binfo};
   for (auto* b : bufs) b->release();
   (void)hipStreamDestroy(c->stream);
   delete c;

@@ -511,77 +511,5 @@ __device__ __forceinline__ void idct_rows(float* tb, uint32_t q, const float* Qt
                                                     0x05040100u));
 }
 
-// idct_rows with a smaller register peak, for the fused decoder, where every
-// lane's 32 coefficient words stay live through the unit loop: the same
-// products and sums in the same order (so the same pixels), but each
-// coefficient word and Q pair loaded at its step, and stage 2 in two halves
-// of four output columns (eight sums live, not sixteen).
-__device__ __forceinline__ void fence8(float (&a)[8]) {
-  asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
-               "+v"(a[7]));
-}
-__device__ __forceinline__ void idct_rows_lean(float* tb, uint32_t q, const float* Qt, uint2& w0, uint2& w1) {
-  const uint32_t* tw = reinterpret_cast<const uint32_t*>(tb);
-  // ---- dequantise and stage 1 (DCT.cpp:331, 256-266), zero rows skipped
-  float Um[16];  // Um[2i + h] = U[i][2q + h]
-#pragma unroll
-  for (int j = 0; j < 16; j++) Um[j] = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t zk = tw[k * 4 + q];
-    if (!__any(zk != 0u)) continue;
-    const float2 qv = *reinterpret_cast<const float2*>(Qt + k * 8 + 2 * q);
-    const float z0 = (float)(int16_t)zk * qv.x;
-    const float z1 = (float)(int16_t)(zk >> 16) * qv.y;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      Um[2 * i] = Um[2 * i] + c_dct[k * 8 + i] * z0;
-      Um[2 * i + 1] = Um[2 * i + 1] + c_dct[k * 8 + i] * z1;
-    }
-    fence16(Um);
-  }
-  wave_sync();  // (the image is read; the transpose rewrites the tile)
-  float P[16];  // P[2k + h] = U[2q + h][k]
-  transpose_tile(tb, q, Um, P);
-  // ---- stage 2 (squareMatrixMul<8>(U, DCT)), columns 0..3 then 4..7, zero
-  // columns skipped; clamp(roundf(R) + 128) (DCT.cpp:358-362) per half
-  uint32_t wr[4];  // w0.x, w1.x, w0.y, w1.y
-#pragma unroll
-  for (int hv = 0; hv < 2; hv++) {
-    float S[8];  // S[2(v - 4 hv) + h] = R[2q + h][v]
-#pragma unroll
-    for (int j = 0; j < 8; j++) S[j] = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      if (!__any(P[2 * k] != 0.0f || P[2 * k + 1] != 0.0f)) continue;
-#pragma unroll
-      for (int v = 0; v < 4; v++) {
-        S[2 * v] = S[2 * v] + P[2 * k] * c_dct[k * 8 + 4 * hv + v];
-        S[2 * v + 1] = S[2 * v + 1] + P[2 * k + 1] * c_dct[k * 8 + 4 * hv + v];
-      }
-      fence8(S);
-    }
-    uint32_t px[8];
-    bool tie = false;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      S[j] = __builtin_amdgcn_fmed3f(S[j], -128.0f, 127.0f);
-      tie = tie || __builtin_amdgcn_fractf(S[j]) == 0.5f;
-      px[j] = bits(S[j] + kMagicPx);
-    }
-    if (tie) {
-#pragma unroll
-      for (int j = 0; j < 8; j++)
-        px[j] = (uint32_t)((int)__builtin_truncf(S[j] + __builtin_copysignf(kHalfDown, S[j])) + 128);
-    }
-    wr[2 * hv] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[6], px[4], 0x0c0c0400u),
-                                       __builtin_amdgcn_perm(px[2], px[0], 0x0c0c0400u), 0x05040100u);
-    wr[2 * hv + 1] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[7], px[5], 0x0c0c0400u),
-                                           __builtin_amdgcn_perm(px[3], px[1], 0x0c0c0400u), 0x05040100u);
-  }
-  w0 = make_uint2(wr[0], wr[2]);
-  w1 = make_uint2(wr[1], wr[3]);
-}
-
 }  // namespace xf
 }  // namespace myyuv_gpu
