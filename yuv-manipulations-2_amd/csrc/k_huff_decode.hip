@@ -49,12 +49,6 @@ constexpr uint32_t kStageQuads = 384;
 // the value needs no select.
 constexpr uint32_t kZeroBit = kStageQuads * 128u;
 
-// the fused decoder's transform: eight lanes per block (1, xf::idct_rows8)
-// or four (0, xf::idct_rows)
-#ifndef MYYUV_DEC_XF8
-#define MYYUV_DEC_XF8 0
-#endif
-
 // diagnostic ablations (never the product; 4: the non-constant blocks'
 // transform replaced by a copy, stores kept): 1 = no symbol decode, 2 = no
 // table parse either, 3 = the fused decoder skips its transform
@@ -592,32 +586,6 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
   const uint32_t rrank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rest >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rest, 0u));
   if (D.live && !isdc) s_blk[rrank] = (uint16_t)lane;  // compacted position -> the block's lane in the group
   float* tile = reinterpret_cast<float*>(stq);
-#if MYYUV_DEC_XF8
-  // eight lanes per block: units of 8 compacted blocks, lane (b8, o) writes
-  // pixel row o of the unit's block b8 (xf::idct_rows8)
-  const uint32_t o = lane & 7u, b8 = lane >> 3;
-#pragma unroll 1
-  for (uint32_t u = 0; 8u * u < nrest; u++) {
-    const bool mine = D.live && !isdc && (rrank >> 3) == u;
-    if (mine) {
-      uint4* img = reinterpret_cast<uint4*>(tile + (rrank & 7u) * xf::kTile);
-#pragma unroll
-      for (int c = 0; c < 8; c++) img[c] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
-    }
-    if (lane < 8u && 8u * u + lane >= nrest) {  // (slots past the last block: zero)
-      uint4* img = reinterpret_cast<uint4*>(tile + lane * xf::kTile);
-#pragma unroll
-      for (int c = 0; c < 8; c++) img[c] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    xf::wave_sync();
-    const uint2 row = xf::idct_rows8(tile + b8 * xf::kTile, o, sq);
-    if (8u * u + b8 < nrest) {
-      const uint32_t gl = D.g0 + s_blk[8u * u + b8];  // the block of compacted position 8u + b8
-      *reinterpret_cast<uint2*>(fr + xf::block_row_offset(U, gl - U.cum, o)) = row;
-    }
-    xf::wave_sync();  // the next unit rewrites the tile
-  }
-#else
   const uint32_t q = lane & 3u, b = lane >> 2;
 #pragma unroll 1
   for (uint32_t u = 0; 16u * u < nrest; u++) {
@@ -655,7 +623,6 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     }
     xf::wave_sync();  // the next unit rewrites the tile
   }
-#endif
 }
 
 }  // namespace myyuv_gpu

@@ -511,70 +511,5 @@ __device__ __forceinline__ void idct_rows(float* tb, uint32_t q, const float* Qt
                                                     0x05040100u));
 }
 
-// K6's body with eight lanes per block (the fused decoder's transform,
-// MYYUV_DEC_XF8): lane (b, o) of an 8-block unit owns column o in stage 1 and
-// row o in stage 2, eight outputs each, so the transform's registers are
-// half of idct_rows's (the decoder keeps every lane's 32 coefficient words
-// live through its unit loop, and this region sets its register peak).  The
-// same products and sums in the same order as idct_rows (DCT.cpp:330-334,
-// :358-362), the same zero-step skipping (per 8-block unit).  tb: the block's
-// tile (its int16 image, natural order, in the first 32 dwords; kTile floats,
-// rows at stride 9); out: pixel row o, 8 bytes.
-__device__ __forceinline__ void fence8(float (&a)[8]) {
-  asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
-               "+v"(a[7]));
-}
-__device__ __forceinline__ uint2 idct_rows8(float* tb, uint32_t o, const float* Qt) {
-  const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tb);
-  // ---- dequantise and stage 1: U[i][o] = sum_k D[k][i] * Z[k][o] * Q[k][o]
-  float Um[8];  // Um[i] = U[i][o]
-#pragma unroll
-  for (int i = 0; i < 8; i++) Um[i] = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t zk = t16[8 * k + o];
-    if (!__any(zk != 0u)) continue;
-    const float z = (float)(int16_t)zk * Qt[8 * k + o];
-#pragma unroll
-    for (int i = 0; i < 8; i++) Um[i] = Um[i] + c_dct[k * 8 + i] * z;
-    fence8(Um);
-  }
-  wave_sync();  // (the image is read; the transpose rewrites the tile)
-#pragma unroll
-  for (int i = 0; i < 8; i++) tb[9 * i + o] = Um[i];
-  wave_sync();
-  float P[8];  // P[k] = U[o][k]
-#pragma unroll
-  for (int k = 0; k < 8; k++) P[k] = tb[9 * o + k];
-  // ---- stage 2: R[o][v] = sum_k U[o][k] * D[k][v]; clamp(roundf(R) + 128)
-  float S[8];
-#pragma unroll
-  for (int v = 0; v < 8; v++) S[v] = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    if (!__any(P[k] != 0.0f)) continue;
-#pragma unroll
-    for (int v = 0; v < 8; v++) S[v] = S[v] + P[k] * c_dct[k * 8 + v];
-    fence8(S);
-  }
-  uint32_t px[8];
-  bool tie = false;
-#pragma unroll
-  for (int v = 0; v < 8; v++) {
-    S[v] = __builtin_amdgcn_fmed3f(S[v], -128.0f, 127.0f);
-    tie = tie || __builtin_amdgcn_fractf(S[v]) == 0.5f;
-    px[v] = bits(S[v] + kMagicPx);
-  }
-  if (tie) {
-#pragma unroll
-    for (int v = 0; v < 8; v++)
-      px[v] = (uint32_t)((int)__builtin_truncf(S[v] + __builtin_copysignf(kHalfDown, S[v])) + 128);
-  }
-  return make_uint2(__builtin_amdgcn_perm(__builtin_amdgcn_perm(px[3], px[2], 0x0c0c0400u),
-                                          __builtin_amdgcn_perm(px[1], px[0], 0x0c0c0400u), 0x05040100u),
-                    __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[7], px[6], 0x0c0c0400u),
-                                          __builtin_amdgcn_perm(px[5], px[4], 0x0c0c0400u), 0x05040100u));
-}
-
 }  // namespace xf
 }  // namespace myyuv_gpu
