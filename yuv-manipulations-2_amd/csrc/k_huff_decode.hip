@@ -49,6 +49,12 @@ constexpr uint32_t kStageQuads = 384;
 // the value needs no select.
 constexpr uint32_t kZeroBit = kStageQuads * 128u;
 
+// parse_table reads the chunk's first 20 bytes into registers at once (1)
+// or every byte from LDS as the group walk reaches it (0)
+#ifndef MYYUV_K5_TABLE_REGS
+#define MYYUV_K5_TABLE_REGS 1
+#endif
+
 // diagnostic ablations (never the product; 4: the non-constant blocks'
 // transform replaced by a copy, stores kept): 1 = no symbol decode, 2 = no
 // table parse either, 3 = the fused decoder skips its transform
@@ -120,14 +126,32 @@ struct Table {
 template <class Chunk>
 __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T) {
   if (s < 3) return 12;
-  const uint32_t nbits = c.byte(0) | (c.byte(1) << 8);
-  const uint32_t tb = c.byte(2);
+#if MYYUV_K5_TABLE_REGS
+  // the chunk's first 20 bytes in registers, loaded together (the group walk
+  // below is a chain of dependent byte reads: from registers, not one LDS
+  // round trip per group; a table of at most 8 symbols ends within them)
+  uint32_t hb[5];
+#pragma unroll
+  for (uint32_t k = 0; k < 5; k++) hb[k] = c.bits32(32u * k);
+  auto byte_at = [&](uint32_t i) -> uint32_t {
+    if (i < 20u) {
+      const uint32_t k = i >> 2;
+      const uint32_t w = k == 0 ? hb[0] : (k == 1 ? hb[1] : (k == 2 ? hb[2] : (k == 3 ? hb[3] : hb[4])));
+      return (w >> (8u * (i & 3u))) & 0xFFu;
+    }
+    return c.byte(i);
+  };
+#else
+  auto byte_at = [&](uint32_t i) -> uint32_t { return c.byte(i); };
+#endif
+  const uint32_t nbits = byte_at(0) | (byte_at(1) << 8);
+  const uint32_t tb = byte_at(2);
   if (nbits > 512 || 3 + tb + (nbits + 7) / 8 > s) return 12;
   uint64_t cnt = 0, glo = 0, ghi = 0;
   uint32_t seen = 0, total = 0, i = 3;
   bool regular = true;
   while (i - 3 < tb) {
-    const uint32_t info = c.byte(i);
+    const uint32_t info = byte_at(i);
     const uint32_t L = (info >> 5) + 1, n = (info & 31) + 1;
     const uint32_t nbytes = (n * 11 + 7) / 8;
     total += n;
