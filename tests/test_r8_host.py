@@ -40,8 +40,8 @@ def harness_san(tmp_path_factory):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
     exe = str(tmp_path_factory.mktemp("r8san") / "r8_host_san")
-    subprocess.run([HIPCC, "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-                    "-fno-gpu-sanitize", "-fno-omit-frame-pointer",
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-fno-gpu-sanitize"]
+    subprocess.run([HIPCC, "-O1", "-g", "-std=c++17"] + san + ["-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
                     "-I", os.path.join(ROOT, "yuv-manipulations-2_amd", "csrc"), "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tools", "r8_host.cpp"), "-o", exe], check=True)
     return exe
