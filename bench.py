@@ -653,8 +653,9 @@ class Run:
             nk = int(self.d_size[f].item())
             if bytes(self.d_pay[f, :nk].cpu().numpy()) != pay0:
                 raise SystemExit(f"frame slot {f}: compressed stream differs from slot 0's")
+        self.want_decode = None
         if isinstance(c, GpuCodec):
-            want = c.codecs[0].decompress(pay0, self.w, self.h, self.q3)
+            want = self.want_decode = c.codecs[0].decompress(pay0, self.w, self.h, self.q3)
             for k in range(self.nf):
                 for b in range(self.B):
                     if bytes(self.d_out[k, b * self.samples:(b + 1) * self.samples].cpu().numpy()) != want:
@@ -669,6 +670,11 @@ class Run:
         self.timing holds this rank's wall / compute / gather-tail seconds and
         gathered bytes, self.gather_bad the ranks whose sizes passed a slot."""
         c = self.codec
+        # every output the timed region checks afterwards (verify_timed) is
+        # cleared first, so nothing the untimed pass wrote can pass for it
+        self.d_pay.zero_()
+        self.d_size.zero_()
+        self.d_out.zero_()
         gat = None
         if self.world > 1:
             import batch
@@ -705,6 +711,50 @@ class Run:
         if self.world > 1:
             dist.barrier()
         return wall, got
+
+    def verify_timed(self, steps):
+        """After the timed region: the streams of its last step and the frames
+        its last decode launches wrote (each context's last launch group),
+        against the pinned bytes / manifest and the host-API decode."""
+        c = self.codec
+        c.sync()
+        js = range((steps - 1) * self.ngroups, steps * self.ngroups)
+        nstream = ndec = 0
+        for j in js:
+            k, _, nb, slot = self.group_desc(j)
+            sizes = self.d_size[slot:slot + nb].cpu().tolist()
+            for b in range(nb):
+                pay = bytes(self.d_pay[slot + b, :sizes[b]].cpu().numpy())
+                if self.name == "batch4k":
+                    m = self.manifest[self.gframes[j % self.ngroups * self.B + b]]
+                    ok = len(pay) == m["payload_size"] and sha(pay) == m["payload_sha"]
+                else:
+                    ok = len(pay) == self.payload0 and (sha(pay) == BIG_RECOMPRESSED_SHA if self.q == 50 else True)
+                if not ok:
+                    raise SystemExit(f"timed region: stream of launch group {j} frame {b} is wrong")
+                nstream += 1
+        last = {}
+        for j in js:  # each context's last launch group decoded into d_out[k]
+            last[self.group_desc(j)[0]] = j
+        for k, j in sorted(last.items()):
+            _, _, nb, _ = self.group_desc(j)
+            decs = hashes(self.d_out[k], nb, self.samples)
+            for b in range(nb):
+                if self.name == "batch4k":
+                    want = self.manifest[self.gframes[j % self.ngroups * self.B + b]]["decoded_sha"]
+                elif self.want_decode is not None:
+                    want = sha(self.want_decode)
+                else:
+                    continue
+                if decs[b] != want:
+                    raise SystemExit(f"timed region: decode of launch group {j} frame {b} is wrong")
+                ndec += 1
+        src = "tests/golden/batch4k_512.json" if self.name == "batch4k" else (
+            f"the pinned reference bytes {BIG_RECOMPRESSED_SHA[:8]}" if self.q == 50 else "the first pass's size")
+        self.verified["timed_region"] = (f"timed-region outputs checked (cleared before it): the last step's "
+                                         f"{nstream} streams == {src}; {ndec} frames of each context's last "
+                                         f"decode == " + ("the manifest" if self.name == "batch4k"
+                                                          else "the host-API decode"))
 
     def verify_gathered(self, got, steps):
         """Rank 0, N > 1: the gathered streams in global frame order."""
@@ -873,6 +923,7 @@ def main(argv=None):
             c.profile(True, kernels=["fdct_quant", "fdct_fix"])
     t, got = run.timed(args.steps, dist, dev, args.gather_chunk)
     checked(codec.check, "the timed region", dist, world, rank, dev, bad_ranks=run.gather_bad)
+    checked(run.verify_timed, "the timed region's outputs", dist, world, rank, dev, args.steps)
     stats = {}
     for c in stamped:
         for kname, (kms, kn) in c.kernel_stats().items():
@@ -901,12 +952,14 @@ def main(argv=None):
         breakdown = c0.kernel_stats()
         c0.profile(False)
     side = None
+    b4 = None
+    if gpu and not args.no_side and name == "chef-big" and run.q == 50:
+        # configs[3]/[4] on every rank (all ranks take part in its gather),
+        # before rank 0's own side work so no rank waits in a collective for it
+        b4 = batch4k_side(args, codec, raw, big, world, rank, dist, dev)
     if gpu and rank == 0 and not args.no_side:
         side = side_measurements(args, run, codec, raw, big, world, dev)
-    if gpu and not args.no_side and name == "chef-big" and run.q == 50:
-        # configs[3]/[4] on every rank (all ranks take part in its gather)
-        b4 = batch4k_side(args, codec, raw, big, world, rank, dist, dev)
-        if side is not None:
+        if b4 is not None:
             side["batch4k"] = b4
 
     if rank == 0:
@@ -1043,6 +1096,7 @@ def batch4k_side(args, codec, raw, big, world, rank, dist, dev):
     checked(run.warmup, "side.batch4k's untimed pass", dist, world, rank, dev, 1)
     t, got = run.timed(passes, dist, dev, a.gather_chunk)
     checked(codec.check, "side.batch4k's timed passes", dist, world, rank, dev, bad_ranks=run.gather_bad)
+    checked(run.verify_timed, "side.batch4k's timed outputs", dist, world, rank, dev, passes)
     out = None
     if world > 1:
         ranks = rank_timings(dist, world, dev, run.timing)
@@ -1051,7 +1105,7 @@ def batch4k_side(args, codec, raw, big, world, rank, dist, dev):
         out = {"value": round(passes * run.n_total * run.mp / t, 2), "unit": "MP/s", "n_gpus": world,
                "scaling": "strong", "frames": run.n_total, "passes": passes,
                "ms_per_pass": round(t / passes * 1e3, 3), "frames_per_launch": run.B,
-               "verified": run.verified["first_pass"]}
+               "verified": run.verified["first_pass"], "verified_timed": run.verified["timed_region"]}
         if world > 1:
             out["verified_gathered"] = run.verify_gathered(got, passes)
             out["max_gather_tail_s"] = round(max(r["gather_tail_s"] for r in ranks), 6)

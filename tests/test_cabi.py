@@ -40,6 +40,16 @@ def test_exported_symbols_are_plain_c():
         assert name in exported, name  # unmangled: extern "C"
 
 
+def test_kernel_ids_match_the_header():
+    """myyuv_hip.KERNELS / K_* (profile and skip masks) follow MYYUV_K_* of the header."""
+    import myyuv_hip
+    ids = {m.group(1): int(m.group(2)) for m in
+           re.finditer(r"^#define MYYUV_K_([A-Z0-9_]+)\s+(\d+)", open(HEADER).read(), re.M)}
+    assert ids.pop("COUNT") == len(myyuv_hip.KERNELS)
+    for name, kid in ids.items():
+        assert getattr(myyuv_hip, "K_" + name) == kid, name
+
+
 def test_error_strings_are_the_reference_messages():
     import myyuv_hip
     assert myyuv_hip.strerror(2) == "Level of quality must be between 1 and 100"

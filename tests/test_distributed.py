@@ -201,6 +201,7 @@ def test_bench_n2_loop_cpu_codec(workload, extra):
     assert d["config"]["frames_per_step"] == 2 * per
     assert f"rank 0 gathered {2 * steps * per} streams" in d["verified"]["gathered"]
     assert "first_pass" in d["verified"]
+    assert d["verified"]["timed_region"].startswith("timed-region outputs checked")
     if workload == "batch4k":
         assert "tests/golden/batch4k_512.json" in d["verified"]["gathered"]
     # per-rank compute and gather time, separately (the N > 1 line's `ranks`)

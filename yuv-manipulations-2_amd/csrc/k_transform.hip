@@ -261,7 +261,11 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
     fdct_load(img, q, xr);
     if (!fdct_fast(xr, tb, q, sqr, U.p, store) && lane == 0) {
       const uint32_t c = MYYUV_FIX_SPREAD ? ua % kFixLists : 0u;
-      fix_list(fix, G, c)[atomicAdd(fix_count(fix, par, c), 1u)] = ua;
+      // (a launch lists each unit at most once, so a count below the list's
+      // capacity is guaranteed while k_fdct_fix resets the counts; the clamp
+      // keeps a stale count, e.g. a diagnostic skip of the fix kernel, in bounds)
+      const uint32_t idx = atomicAdd(fix_count(fix, par, c), 1u);
+      if (idx < (nall + kFixLists - 1) / kFixLists) fix_list(fix, G, c)[idx] = ua;
     }
 #endif
   }

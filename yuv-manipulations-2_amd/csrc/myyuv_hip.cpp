@@ -197,7 +197,11 @@ struct myyuv_hip_ctx {
   uint32_t fix_par = 0;
   uint32_t xf_resident[2] = {kXfWaves / 4, kXfWaves / 4};  // K1, K6 workgroups resident on the device
   uint32_t fix_resident = kXfWaves / 4;                      // k_fdct_fix workgroups resident
-  uint32_t fix_grid = 64;  // k_fdct_fix's grid at qualities up to fix_qmax (MYYUV_FIX_GRID, 0: resident)
+  // k_fdct_fix's grid at qualities up to fix_qmax (MYYUV_FIX_GRID; 0, the
+  // default: the resident count, as above fix_qmax).  A small fixed grid
+  // measured no faster (profiles/r4h_fix_ab.txt), and busy content at low q
+  // can list far more units than the bench frame's 0.07 %.
+  uint32_t fix_grid = 0;
   uint32_t fix_qmax = 75;  // (MYYUV_FIX_QMAX)
   // encoder: K1 -> K2 through HBM (split), or the fused single-pass kernel
   // k_encode_tile (MYYUV_ENCODER=fused|split)
@@ -434,11 +438,12 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
 }
 
 // K1, then its exact path for the units it listed (k_fdct_fix).  The list
-// is on the device, so the fix grid cannot follow its length: fix_grid
-// workgroups (4 waves each) where the quality keeps it short, the resident
-// count otherwise (the fast path fails for 0.07 % of the bench frame's units
-// at q50, 18 % at q90, 48 % at q100: tools/diag/fast_dct_sim.py); workgroups
-// past the list return at once.  k2ctl: K2's overflow count, zeroed by K1
+// is on the device, so the fix grid cannot follow its length: the resident
+// count (the fast path fails for 0.07 % of the bench frame's units at q50,
+// 18 % at q90, 48 % at q100, more on noise: tools/diag/fast_dct_sim.py);
+// workgroups past the list return at once.  MYYUV_FIX_GRID=n caps it at n
+// workgroups for qualities up to MYYUV_FIX_QMAX (a test of the grid-stride
+// walk).  k2ctl: K2's overflow count, zeroed by K1
 // (nullptr: none).
 int launch_fdct(myyuv_hip_ctx* c, const FrameGeom& G, const uint8_t* in, const QTables* qt, uint32_t* k2ctl,
                 hipStream_t s) {
@@ -456,6 +461,10 @@ int launch_fdct(myyuv_hip_ctx* c, const FrameGeom& G, const uint8_t* in, const Q
   const uint32_t grid = std::max(per, (want * 4 / kFixWaves) / per * per);
   e |= launch(c, MYYUV_K_FDCT_FIX, k_fdct_fix, dim3(grid), dim3(64 * kFixWaves), s, in, G, qt, c->coef.as<uint4>(),
               c->rmask.as<uint8_t>(), c->binfo.as<uint32_t>(), c->sink.as<uint4>(), c->fix.as<uint32_t>(), par);
+  // the fix kernel zeroes the next launch's counts; without it (a diagnostic
+  // skip, or a failed launch) the host does
+  if (e || ((c->skip >> MYYUV_K_FDCT_FIX) & 1u))
+    e |= hipMemsetAsync(fix_count(c->fix.as<uint32_t>(), par ^ 1u, 0), 0, kFixLists * 32 * 4, s) != hipSuccess;
   return e;
 }
 

@@ -22,8 +22,9 @@ E_BMP_INVALID, E_BMP_SIGN, E_BMP_UNSUPPORTED = 15, 16, 17
 KERNELS = ["fdct_quant", "huff_encode", "scan_tiles", "stream_out", "encode_tile", "huff_decode",
            "dequant_idct", "huff_encode_wide", "huff_encode_r16", "huff_encode_wave", "bmp_to_iyuv",
            "fdct_fix"]
+# ids: MYYUV_K_* of include/myyuv_hip.h, in KERNELS order (tests/test_cabi.py checks both)
 (K_FDCT, K_HUFF_ENC, K_SCAN, K_COMPACT, K_ENCODE_TILE, K_HUFF_DEC, K_IDCT, K_HUFF_WIDE,
- K_HUFF_R16, K_HUFF_WAVE, K_BMP) = range(11)
+ K_HUFF_R16, K_HUFF_WAVE, K_BMP, K_FDCT_FIX) = range(len(KERNELS))
 
 # the exported symbols include/myyuv_hip.h declares (checked by the CPU tests)
 EXPORTS = [
