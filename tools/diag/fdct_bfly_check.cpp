@@ -1,0 +1,102 @@
+/* Diagnostic + test harness (CPU, test infrastructure): K1's butterfly fast
+ * path (xform_common.hpp fdct_fast, round 5) emulated operation for operation
+ * in IEEE binary32 (gcc -ffp-contract=off, explicit fmaf), against the
+ * reference transform (myyuv_DCT/DCT.cpp:232-254, 269-277: k-ascending sums of
+ * rounded products, roundf(Y / Q)).  Per 16-block unit: the fast path's
+ * bound test (beta_h = A * kb[row], kb = K * max_v r[row][v]); a unit that
+ * passes must equal the reference in every coefficient (any mismatch is a
+ * failure of the bound: exit 1).  Counts the units the exact path must take.
+ *
+ * stdin: u32 nblocks, then per block 64 u8 pixels (row-major) + u8 plane id;
+ * then 3 x 64 f32 Q tables (natural order).  Units are 16 consecutive blocks
+ * of one plane (the caller orders them that way).
+ * stdout: "units <n> exact <m> mismatches <k> outputs <o>"
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static const float Dm[64] = {
+    0.3535533845424652f,   0.3535533845424652f,  0.3535533845424652f,  0.3535533845424652f,
+    0.3535533845424652f,   0.3535533845424652f,  0.3535533845424652f,  0.3535533845424652f,
+    0.4903925955295563f,   0.4157347679138184f,  0.277785062789917f,   0.09754510968923569f,
+    -0.09754515439271927f, -0.2777851521968842f, -0.4157347977161407f, -0.4903926253318787f,
+    0.4619397222995758f,   0.1913416981697083f,  -0.1913417428731918f, -0.4619397819042206f,
+    -0.4619397222995758f,  -0.1913415491580963f, 0.1913417875766754f,  0.4619397521018982f,
+    0.4157347679138184f,   -0.09754515439271927f, -0.4903926253318787f, -0.2777849733829498f,
+    0.2777851819992065f,   0.4903925955295563f,  0.09754502773284912f, -0.4157348573207855f,
+    0.3535533547401428f,   -0.3535533547401428f, -0.353553295135498f,  0.3535534739494324f,
+    0.3535533547401428f,   -0.3535535931587219f, -0.3535532355308533f, 0.3535533845424652f,
+    0.277785062789917f,    -0.4903926253318787f, 0.09754519909620285f, 0.4157346487045288f,
+    -0.4157348573207855f,  -0.09754510223865509f, 0.4903926253318787f, -0.2777853906154633f,
+    0.1913416981697083f,   -0.4619397222995758f, 0.4619397521018982f,  -0.1913419365882874f,
+    -0.1913414746522903f,  0.4619396328926086f,  -0.4619398415088654f, 0.1913419365882874f,
+    0.09754510968923569f,  -0.2777849733829498f, 0.4157346487045288f,  -0.4903925657272339f,
+    0.4903926849365234f,   -0.4157347679138184f, 0.2777855396270752f,  -0.09754576534032822f};
+
+#include "../../yuv-manipulations-2_amd/csrc/fdct_bfly.h"
+using namespace myyuv_bfly;
+
+/* reference: T = D X, Y = T D^T, roundf(Y / Q) (DCT.cpp:232-254, 269-277) */
+static void ref_block(const uint8_t* px, const float* Q, int16_t* out) {
+  float X[64], T[64], Y[64];
+  for (int i = 0; i < 64; i++) X[i] = (float)((int)px[i] - 128);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) {
+      float s = 0.0f;
+      for (int k = 0; k < 8; k++) s = s + Dm[i * 8 + k] * X[k * 8 + j];
+      T[i * 8 + j] = s;
+    }
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) {
+      float s = 0.0f;
+      for (int k = 0; k < 8; k++) s = s + T[i * 8 + k] * Dm[j * 8 + k];
+      Y[i * 8 + j] = s;
+    }
+  for (int i = 0; i < 64; i++) out[i] = (int16_t)roundf(Y[i] / Q[i]);
+}
+
+int main(void) {
+  uint32_t n;
+  if (fread(&n, 4, 1, stdin) != 1) return 2;
+  uint8_t* px = (uint8_t*)malloc((size_t)n * 65);
+  if (fread(px, 65, n, stdin) != n) return 2;
+  float Q[3][64], R[3][64], KB[3][8];
+  if (fread(Q, 4, 192, stdin) != 192) return 2;
+  for (int p = 0; p < 3; p++) {
+    for (int i = 0; i < 64; i++) R[p][i] = 1.0f / Q[p][i];
+    bfly_row_bounds(R[p], KB[p]);
+  }
+  long units = 0, exact = 0, mism = 0, outputs = 0;
+  for (uint32_t u0 = 0; u0 < n; u0 += 16) {
+    const uint32_t nb = n - u0 < 16 ? n - u0 : 16;
+    int ok = 1;
+    int16_t fast[16][64];
+    for (uint32_t b = 0; b < nb; b++) {
+      const uint8_t* blk = px + (size_t)(u0 + b) * 65;
+      const int p = blk[64];
+      ok &= bfly_block(blk, R[p], KB[p], fast[b]);
+    }
+    units++;
+    if (!ok) {
+      exact++;
+      continue;
+    }
+    for (uint32_t b = 0; b < nb; b++) {
+      const uint8_t* blk = px + (size_t)(u0 + b) * 65;
+      int16_t ref[64];
+      ref_block(blk, Q[blk[64]], ref);
+      for (int i = 0; i < 64; i++) {
+        outputs++;
+        if (ref[i] != fast[b][i]) {
+          if (mism < 10) fprintf(stderr, "mismatch block %u coef %d: fast %d ref %d\n", u0 + b, i, fast[b][i], ref[i]);
+          mism++;
+        }
+      }
+    }
+  }
+  printf("units %ld exact %ld mismatches %ld outputs %ld\n", units, exact, mism, outputs);
+  return mism ? 1 : 0;
+}

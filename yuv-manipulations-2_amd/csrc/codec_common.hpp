@@ -139,6 +139,7 @@ __host__ __device__ __forceinline__ uint32_t block_row(const FrameGeom& G, int p
 struct QTables {
   float q[3][64];     // natural order, DCT.cpp:286-290
   float r[3][64];     // 1.0f / q, correctly rounded (K1's division-free fast path)
+  float kb[3][8];     // K1's fast-path bound per row (fdct_bfly.h bfly_row_bounds)
 };
 
 // K1's near-tie window per unit of |t| (k_transform.hip): t = y * fl(1/Q)

@@ -1317,7 +1317,7 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
   using namespace xf;
   __shared__ uint4 s_img[8 * kK2Group];
   __shared__ float s_tile[kTileWaves][kXfUnit * kTile];
-  __shared__ float s_q[2 * 3 * 64];
+  __shared__ float s_q[kSqWords];  // QTables::q, r, kb
   __shared__ uint8_t s_rmk[kK2Group];
   static_assert(sizeof(TileScratch) <= sizeof(s_tile), "K2 scratch over the transpose tiles");
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1328,7 +1328,7 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
   tile_geometry(G, T, f, t, p, g0, nloc);
   TileRows rows;
   load_tile_rows(frame, G, T, wave, b, q, rows);
-  stage_tables<2 * 3 * 64>(qt->q[0], s_q);
+  stage_tables<kSqWords>(qt->q[0], s_q);
   float* tb = s_tile[wave] + b * kTile;
   uint8_t* img = reinterpret_cast<uint8_t*>(tb);
   // ---- phase 1

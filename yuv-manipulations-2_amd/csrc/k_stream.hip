@@ -232,8 +232,16 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
                                                     uint8_t* __restrict__ out, uint32_t cap) {
   __shared__ uint32_t s_wt[4], s_hdr[4];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t t = blockIdx.x, f = blockIdx.y, ntile = G.tcum[3];
-  const uint32_t T = f * ntile + t;
+  const uint32_t ntile = G.tcum[3];
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and
+  // b + 8 share one L2), and a K2 window's kWinTiles tiles read interleaved
+  // pieces of the same stage lines, so they go to one XCD: workgroup L takes
+  // batch tile kWinTiles * (8 * (L / (8 kWinTiles)) + L % 8) + (L / 8) %
+  // kWinTiles (a bijection on the grid, a multiple of 8 * kWinTiles)
+  const uint32_t L = blockIdx.x, slot = L >> 3;
+  const uint32_t T = kWinTiles * ((slot / kWinTiles) * 8u + (L & 7u)) + slot % kWinTiles;
+  if (T >= ntile * G.nframes) return;
+  const uint32_t f = T / ntile, t = T - f * ntile;
   const int p = tile_plane(G, t);
   const uint32_t g0 = tile_first(G, p, t);
   const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);

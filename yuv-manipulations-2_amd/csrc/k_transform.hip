@@ -165,19 +165,16 @@ __device__ __forceinline__ void stage_zz(uint4* szz) {
   if (threadIdx.x < 32) reinterpret_cast<uint32_t*>(szz)[threadIdx.x] = kZzPairs.v[threadIdx.x];
 }
 
-// K1's exact path out of line (MYYUV_K1_INLINE_EXACT 0): a unit whose fast
-// result is not provably the reference's is appended by K1 to one of
-// kFixLists lists (unit ua to list ua % kFixLists, fix_count / fix_list in
-// codec_common.hpp; each launch uses the counts of its parity `par`) and
-// transformed by k_fdct_fix, which runs next in the stream.  Kept in K1, the
-// exact path's code raised K1 from 64 to 99 VGPRs (7 -> 5 waves per SIMD) and
-// cost it 15 % (profiles/r4g_*).  One count for all units serialised the
-// appends on one address (at q90, 18 % of the units: 47k atomics per
-// 8192x8192 frame, K1 83 -> 215 us); a per-wave register list flushed 64 at a
-// time fixed that but cost K1 4 % at q50 (profiles/r4r_*).
-#ifndef MYYUV_K1_INLINE_EXACT
-#define MYYUV_K1_INLINE_EXACT 0
-#endif
+// K1's exact path out of line: a unit whose fast result is not provably the
+// reference's is appended by K1 to one of kFixLists lists (unit ua to list
+// ua % kFixLists, fix_count / fix_list in codec_common.hpp; each launch uses
+// the counts of its parity `par`) and transformed by k_fdct_fix, which runs
+// next in the stream.  Kept in K1, the exact path's code raised K1 from 64 to
+// 99 VGPRs (7 -> 5 waves per SIMD) and cost it 15 % (profiles/r4g_*).  One
+// count for all units serialised the appends on one address (at q90, 18 % of
+// the units: 47k atomics per 8192x8192 frame, K1 83 -> 215 us); a per-wave
+// register list flushed 64 at a time fixed that but cost K1 4 % at q50
+// (profiles/r4r_*).
 #ifndef MYYUV_FIX_SPREAD
 #define MYYUV_FIX_SPREAD 1  // (0, A/B builds only: every unit in list 0)
 #endif
@@ -195,11 +192,12 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
   // K2's overflow count for the launch that follows in the stream (nullptr: none)
   if (k2ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *k2ctl = 0u;
   __shared__ float tile[4][kXfUnit * kTile];
-  __shared__ float sqr[2 * 3 * 64];  // QTables::q then QTables::r
+  __shared__ float sqr[kSqWords];  // QTables::q, r, kb
   __shared__ uint4 szz[8];
-  static_assert(offsetof(QTables, r) == sizeof(float) * 3 * 64, "layout");
+  static_assert(offsetof(QTables, r) == sizeof(float) * kSqR && offsetof(QTables, kb) == sizeof(float) * kSqKb,
+                "layout");
   stage_zz(szz);
-  stage_tables<2 * 3 * 64>(qt->q[0], sqr);
+  stage_tables<kSqWords>(qt->q[0], sqr);
   if (kSinkSlots > 1) sink += (size_t)((blockIdx.x * 4u + (threadIdx.x >> 6)) % kSinkSlots) * kSinkQuads;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t q = lane & 3u, b = lane >> 2;  // quarter, block in the unit
@@ -254,9 +252,6 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
     auto store = [&](const uint32_t (&c)[16]) {
       store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
     };
-#if MYYUV_K1_INLINE_EXACT
-    fdct_core(img, tb, q, sqr, U.p, store);
-#else
     uint32_t xr[4];
     fdct_load(img, q, xr);
     if (!fdct_fast(xr, tb, q, sqr, U.p, store) && lane == 0) {
@@ -267,7 +262,6 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
       const uint32_t idx = atomicAdd(fix_count(fix, par, c), 1u);
       if (idx < (nall + kFixLists - 1) / kFixLists) fix_list(fix, G, c)[idx] = ua;
     }
-#endif
   }
 }
 

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "codec_common.hpp"
+#include "fdct_bfly.h"
 #include "k_chain.hpp"
 #include "k_stream.hpp"
 #include "myyuv_hip.h"
@@ -87,10 +88,12 @@ void make_qtable(int q, bool chroma, float out[64]) {
   for (int i = 0; i < 64; i++) out[i] = std::min(std::max(std::roundf(base[i] * mul), 1.0f), 255.0f);
 }
 
-// Reciprocals and K1's per-lane near-tie thresholds from the Q tables.
+// Reciprocals and K1's fast-path row bounds from the Q tables.
 void finish_qtables(QTables& t, int planes) {
-  for (int p = 0; p < planes; p++)
+  for (int p = 0; p < planes; p++) {
     for (int n = 0; n < 64; n++) t.r[p][n] = 1.0f / t.q[p][n];
+    myyuv_bfly::bfly_row_bounds(t.r[p], t.kb[p]);
+  }
 }
 
 struct DevBuf {
@@ -493,7 +496,7 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   }
   e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(256), s, c->tinfo.as<uint32_t>(), G,
               static_cast<uint8_t*>(d_out), cap, d_size, err);
-  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(G.tcum[3], nf), dim3(256), s,
+  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(ceil_div(G.tcum[3] * nf, 8 * kWinTiles) * 8 * kWinTiles), dim3(256), s,
               c->stage.as<const uint32_t>(), c->tinfo.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
               c->srcoff.as<const uint32_t>(), c->oslots.as<const uint32_t>(), G, static_cast<uint8_t*>(d_out),
               cap);

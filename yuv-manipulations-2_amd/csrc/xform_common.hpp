@@ -6,6 +6,7 @@
 #include <stddef.h>
 
 #include "codec_common.hpp"
+#include "fdct_bfly.h"
 
 namespace myyuv_gpu {
 namespace xf {
@@ -133,22 +134,8 @@ __device__ __forceinline__ uint32_t unit_stride() { return gridDim.x * 4u; }
 // kSkip: a step k whose P[2k], P[2k+1] are zero in every lane of the wave is
 // skipped (the sums start at +0 and a +-0 product leaves a sum unchanged, so
 // the result is bit-identical; see K6).
-template <bool kInverse, bool kSkip = false, bool kFma = false>
+template <bool kInverse, bool kSkip = false>
 __device__ __forceinline__ void dot_rows(const float (&P)[16], float (&out)[16]) {
-  static_assert(!(kSkip && kFma), "the FMA form is the forward fast path only");
-  if (kFma) {  // the fast path's chain: one rounding per term (bounded against the reference, fdct_core)
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-#pragma unroll
-      for (int v = 0; v < 8; v++) {
-        const float d = c_dct[kInverse ? k * 8 + v : v * 8 + k];
-        out[2 * v] = k == 0 ? P[0] * d : __builtin_fmaf(P[2 * k], d, out[2 * v]);
-        out[2 * v + 1] = k == 0 ? P[1] * d : __builtin_fmaf(P[2 * k + 1], d, out[2 * v + 1]);
-      }
-      fence16(out);
-    }
-    return;
-  }
   if (kSkip) {
 #pragma unroll
     for (int j = 0; j < 16; j++) out[j] = 0.0f;
@@ -235,127 +222,112 @@ __device__ __forceinline__ void load_quads(const uint4* __restrict__ coef, const
 }
 
 
-// Stage 1 of the forward transform for lane (b, q): T[2i + c] = T[i][2q + c] =
-// sum_k D[i][k] * X[k][2q + c] (squareMatrixMul<8>(DCT, X), DCT.cpp:232-242)
-// from the lane's pixel columns xr (signed bytes, row pairs): the reference's
-// order and roundings (kFma false), or an FMA chain (the fast path).
-template <bool kFma>
-__device__ __forceinline__ void fdct_stage1(const uint32_t (&xr)[4], float (&T)[16]) {
+// Stage 1 of the forward transform for lane (b, q), the reference's order
+// and roundings: T[2i + c] = T[i][2q + c] = sum_k D[i][k] * X[k][2q + c]
+// (squareMatrixMul<8>(DCT, X), DCT.cpp:232-242) from the lane's pixel
+// columns xr (unsigned bytes, row pairs; x - 128 as the signed byte x ^ 0x80,
+// DCT.cpp:303).
+__device__ __forceinline__ void fdct_stage1_exact(const uint32_t (&xr)[4], float (&T)[16]) {
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    const float x0 = sbyte(xr[k >> 1], 2 * (k & 1)), x1 = sbyte(xr[k >> 1], 2 * (k & 1) + 1);
+    const uint32_t w = xr[k >> 1] ^ 0x80808080u;
+    const float x0 = sbyte(w, 2 * (k & 1)), x1 = sbyte(w, 2 * (k & 1) + 1);
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const float d = c_dct[i * 8 + k];
-      if (kFma) {
-        T[2 * i] = k == 0 ? d * x0 : __builtin_fmaf(d, x0, T[2 * i]);
-        T[2 * i + 1] = k == 0 ? d * x1 : __builtin_fmaf(d, x1, T[2 * i + 1]);
-      } else {
-        const float p0 = d * x0, p1 = d * x1;
-        T[2 * i] = k == 0 ? p0 : T[2 * i] + p0;
-        T[2 * i + 1] = k == 0 ? p1 : T[2 * i + 1] + p1;
-      }
+      const float p0 = d * x0, p1 = d * x1;
+      T[2 * i] = k == 0 ? p0 : T[2 * i] + p0;
+      T[2 * i + 1] = k == 0 ? p1 : T[2 * i + 1] + p1;
     }
     fence16(T);
   }
 }
-
-// Bound of |Y_fast - Y_ref| for the fast forward path (FMA chains in both
-// stages) against the reference's products and sums (recursive dot products,
-// Higham's gamma_8 bound per stage, |D| <= 0.5):
-//   |T_fast[i][k] - T_ref[i][k]| <= 2 g8 dmax A_k   (A_k = sum_m |X[m][k]|)
-//   |Y_fast[i][v] - Y_ref[i][v]| <= 2 g8 dmax (S_i + dmax A) (1 + g8)
-// with S_i = sum_k |T_fast[i][k]| and A = sum |X| over the block; kFastBound
-// = 2 g8 dmax (1 + 2^-10) (g8 = 8u / (1 - 8u), u = 2^-24; 4.7730e-7), rounded
-// up, which also covers the float evaluation of S_i and of the bound itself.
-constexpr float kFastBound = 4.79e-7f;
 
 // Forward transform + quantisation of lane (b, q)'s part of one block of a
 // 16-block unit (K1's per-unit body, DCT.cpp:269-277, :297-306), in three
 // pieces: fdct_load (the lane's pixel columns from the block's 8 x 8 B image
 // img, which aliases its transpose tile tb), fdct_fast and fdct_exact.  The
 // lane's 16 coefficients go to emit(c): c[2v + h] holds, in its low 16 bits,
-// the int16 coefficient of row 2q + h, column v.  sqr: the Q tables then
-// their reciprocals (QTables layout), p the plane.
+// the int16 coefficient of row 2q + h, column v.  sqr: the Q tables, their
+// reciprocals and the fast path's row bounds (QTables layout), p the plane.
 //
-// Fast path (round 4): both stages as FMA chains (8 instructions per output
-// and stage instead of 15), then t = Y * fl(1/Q) rounded with the magic add.
-// Exactness: the reference's coefficient is roundf(fl(Y_ref / Q)).  With
-// |Y_fast - Y_ref| <= B (kFastBound, per row) and |fl(Y_ref / Q) - t| <=
-// B * r * (1 + 2^-20) + |t| * 2^-21 =: beta (the divide's and the
-// reciprocal's roundings in the second term), every output whose t lies
-// further than beta from the nearest half-integer rounds to the reference's
-// integer: fl(Y_ref / Q) is then strictly inside the same (n - 1/2, n + 1/2).
-// If any output of the wave's unit is closer, fdct_fast emits nothing and
-// returns false (wave-uniform), and the unit goes through fdct_exact: the
-// reference's order, quantised as before (the near-tie lanes with the
-// reference's divide).  On the bench frame (4032x3008, q=50) 12 of 17,766
-// units take the exact path (0.07 %; 18 % at q=90, 48 % at q=100;
-// tools/diag/fast_dct_sim.py).
+// Fast path (round 5): both stages as even/odd butterflies over a nominal
+// basis (fdct_bfly.h: 4.5 instructions per output and stage against round
+// 4's 8-term FMA chains and the reference's 15 operations), then t = Y *
+// fl(1/Q) rounded with the magic add.  fdct_bfly.h bounds |t - fl(Y_ref /
+// Q)| by beta_h = A * kb[row] (A: the block's sum of |x - 128|); every output
+// further than beta_h from the nearest half-integer rounds to the reference's
+// coefficient.  If any output of the wave's unit is closer, fdct_fast emits
+// nothing and returns false (wave-uniform), and the unit goes through
+// fdct_exact: the reference's order, quantised as before (the near-tie lanes
+// with the reference's divide).  On the bench frame (4032x3008, q=50) 14 of
+// 17,766 units take the exact path (0.08 %; 20 % at q=90, 52 % at q=100;
+// tools/diag/fdct_bfly_check.cpp, which also checks every passing unit
+// against the reference transform).
 
-// The lane's columns 2q, 2q+1 of the block's 8 rows; x ^ 0x80 is x - 128 as
-// a signed byte (DCT.cpp:303).  xr[m]: rows 2m (low half), 2m+1 (high half).
-// The image may be overwritten after this (the wave_sync).
+// The lane's columns 2q, 2q+1 of the block's 8 rows, as unsigned pixels:
+// xr[m] = rows 2m (low half), 2m+1 (high half).  The image may be overwritten
+// after this (the wave_sync).
 __device__ __forceinline__ void fdct_load(const uint8_t* img, uint32_t q, uint32_t (&xr)[4]) {
 #pragma unroll
   for (int m = 0; m < 4; m++)
-    xr[m] = (*reinterpret_cast<const uint16_t*>(img + 16 * m + 2 * q) |
-             ((uint32_t)*reinterpret_cast<const uint16_t*>(img + 16 * m + 8 + 2 * q) << 16)) ^
-            0x80808080u;
+    xr[m] = *reinterpret_cast<const uint16_t*>(img + 16 * m + 2 * q) |
+            ((uint32_t)*reinterpret_cast<const uint16_t*>(img + 16 * m + 8 + 2 * q) << 16);
   wave_sync();
 }
+
+// QTables offsets in the staged LDS copy (sqr): q, r, kb
+constexpr int kSqR = 3 * 64, kSqKb = 2 * 3 * 64, kSqWords = 2 * 3 * 64 + 3 * 8;
 
 template <class Emit>
 __device__ __forceinline__ bool fdct_fast(const uint32_t (&xr)[4], float* tb, uint32_t q, const float* sqr, int p,
                                           Emit&& emit) {
-  // ---- A = sum |x| over the block (exact: byte SADs against 128, the
+  // ---- A = sum |x - 128| over the block (exact: byte SADs against 128, the
   // block's four lanes summed)
   uint32_t a = 0;
 #pragma unroll
-  for (int m = 0; m < 4; m++) a = __builtin_amdgcn_sad_u8(xr[m] ^ 0x80808080u, 0x80808080u, a);
+  for (int m = 0; m < 4; m++) a = __builtin_amdgcn_sad_u8(xr[m], 0x80808080u, a);
   a += quad_xor1(a);
   a += quad_xor2(a);
-  // ---- stage 1 (fast), transpose: columns (2q, 2q+1) in, rows (2q, 2q+1) out
+  // ---- stage 1: the lane's two columns (exact integer butterflies, then
+  // the basis products), T[2i + c] = T[i][2q + c]
   float T[16];
-  fdct_stage1<true>(xr, T);
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    float px[8], t[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) px[m] = (float)((xr[m >> 1] >> (8 * (2 * (m & 1) + c))) & 0xFFu);
+    myyuv_bfly::bfly_cols(px, t);
+#pragma unroll
+    for (int i = 0; i < 8; i++) T[2 * i + c] = t[i];
+  }
   float P[16];  // P[2k + h] = T[2q + h][k]
   transpose_tile(tb, q, T, P);
-  float s0 = 0.0f, s1 = 0.0f;  // S_h = sum_k |T[2q + h][k]|
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    s0 += __builtin_fabsf(P[2 * k]);
-    s1 += __builtin_fabsf(P[2 * k + 1]);
-  }
-  // ---- stage 2 (fast): Y[i][v] = sum_k T[i][k] * D[v][k] (squareMatrixMulT<8>(T, DCT),
-  // DCT.cpp:244-254); coef = (int16)roundf(Y / Q) (DCT.cpp:273-276).  One
-  // column pair at a time, quantised as it is done (only P and two sums live;
-  // K1 292 against 334 us per 24-frame launch with all 16 sums in flight)
-  const float af = 0.5f * (float)a;
-  const float b0 = kFastBound * (s0 + af) * (1.0f + 0x1p-20f), b1 = kFastBound * (s1 + af) * (1.0f + 0x1p-20f);
-  // reciprocals of rows 2q, 2q+1 (natural 16q .. 16q + 15)
-  const float* Rq = sqr + 3 * 64 + p * 64 + 16u * q;
+  // ---- stage 2: the lane's two rows, each quantised as it is done:
+  // coef = (int16)roundf(Y / Q) (DCT.cpp:273-276) as rint(Y * fl(1/Q)) where
+  // no output lies within beta_h of a half-integer
+  const float af = (float)a;
+  const float* Rq = sqr + kSqR + p * 64 + 16u * q;  // reciprocals of rows 2q, 2q+1
   uint32_t c[16];
-  float mx = 0.0f;  // max over the lane of |e| + beta: >= 0.5 when an output may round otherwise
+  float mx = 0.0f;  // max over the lane's rows of max |e| + beta_h: >= 0.5 when an output may round otherwise
 #pragma unroll
-  for (int v = 0; v < 8; v++) {
-    float y0 = P[0] * c_dct[v * 8], y1 = P[1] * c_dct[v * 8];
+  for (int h = 0; h < 2; h++) {
+    float x[8], y[8];
 #pragma unroll
-    for (int k = 1; k < 8; k++) {
-      y0 = __builtin_fmaf(P[2 * k], c_dct[v * 8 + k], y0);
-      y1 = __builtin_fmaf(P[2 * k + 1], c_dct[v * 8 + k], y1);
+    for (int k = 0; k < 8; k++) x[k] = P[2 * k + h];
+    myyuv_bfly::bfly_rows(x, y);
+    float em = 0.0f;
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+      const float t = y[v] * Rq[8 * h + v];
+      const float u = t + kMagic;
+      const float e = t - (u - kMagic);
+      em = __builtin_fmaxf(em, __builtin_fabsf(e));
+      c[2 * v + h] = bits(u);
     }
-    const float r0 = Rq[v], r1 = Rq[8 + v];
-    const float t0 = y0 * r0, t1 = y1 * r1;
-    const float u0 = t0 + kMagic, u1 = t1 + kMagic;
-    const float e0 = t0 - (u0 - kMagic), e1 = t1 - (u1 - kMagic);
-    mx = __builtin_fmaxf(mx, __builtin_fmaf(b0, r0, __builtin_fmaf(__builtin_fabsf(t0), kNearRel, __builtin_fabsf(e0))));
-    mx = __builtin_fmaxf(mx, __builtin_fmaf(b1, r1, __builtin_fmaf(__builtin_fabsf(t1), kNearRel, __builtin_fabsf(e1))));
-    c[2 * v] = bits(u0);
-    c[2 * v + 1] = bits(u1);
+    mx = __builtin_fmaxf(mx, __builtin_fmaf(af, sqr[kSqKb + p * 8 + 2 * q + h], em));
   }
-#ifndef MYYUV_FAST_ONLY  // (tuning builds only: no exact path, results may differ)
   if (__builtin_amdgcn_ballot_w64(mx >= 0.5f) != 0) return false;
-#endif
   emit(c);  // every output clears the bound: its rounded t is the reference's coefficient
   return true;
 }
@@ -367,13 +339,13 @@ __device__ __forceinline__ void fdct_exact(const uint32_t (&xr)[4], float* tb, u
                                            Emit&& emit) {
   const uint32_t n0 = 16u * q;
   float T[16];
-  fdct_stage1<false>(xr, T);
+  fdct_stage1_exact(xr, T);
   float P[16];  // P[2k + h] = T[2q + h][k]
   transpose_tile(tb, q, T, P);
   float Y[16];  // Y[2v + h] = Y[2q + h][v]
   dot_rows<false>(P, Y);
   // reciprocals of rows 2q, 2q+1 (natural n0 .. n0 + 15)
-  const float4* R4 = reinterpret_cast<const float4*>(sqr + 3 * 64 + p * 64 + n0);
+  const float4* R4 = reinterpret_cast<const float4*>(sqr + kSqR + p * 64 + n0);
   const float4 r0 = R4[0], r1 = R4[1], r2 = R4[2], r3 = R4[3];
   const float rr[16] = {r0.x, r2.x, r0.y, r2.y, r0.z, r2.z, r0.w, r2.w,
                         r1.x, r3.x, r1.y, r3.y, r1.z, r3.z, r1.w, r3.w};  // [2v + h]
