@@ -125,7 +125,7 @@ int myyuv_gpu_dct_decompress_device(myyuv_hip_handle h, const void* d_payload,
  * (8 B: the CAP-16 tier's list and its rest list), the sizes and row masks
  * (2 B), K1's per-block words for K2 (4 B) and its exact-path list (0.25 B).
  * A 4032x3008 frame (284,256 blocks) takes ~134 MB: the bench's 24-frame
- * launch groups ~3.2 GB per context, 3 contexts ~9.6 GB; a 16-frame
+ * launch groups ~3.2 GB per context, its 4 contexts ~12.8 GB; a 16-frame
  * 8192x8192 batch ~11.9 GB (of 288 GB). */
 int myyuv_hip_reserve_batch(myyuv_hip_handle h, uint32_t width, uint32_t height, uint32_t nframes);
 int myyuv_gpu_dct_compress_batch_device(myyuv_hip_handle h, const void* d_iyuv, uint32_t nframes,

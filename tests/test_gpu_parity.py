@@ -86,26 +86,33 @@ def test_noise_vs_oracle(codec, oracle, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("q", [(90, 90, 90), (100, 100, 100)])
-def test_fdct_unproven_units_listed_in_batches(oracle, q):
-    """K1 keeps the units its fast path cannot prove in one register per wave
-    and lists them 64 at a time (k_transform.hip).  A K1 grid of 1 % of the
-    resident workgroups (MYYUV_K1_GRID_PCT) gives each wave hundreds of units
-    of a noise batch at q90/q100, where a third to a half of them are
-    unproven, so the in-loop flush and the final one both run; every frame
-    must equal the oracle's."""
+@pytest.mark.parametrize("q,fix_grid", [((90, 90, 90), None), ((100, 100, 100), None),
+                                        ((50, 50, 50), "8"), ((75, 75, 75), "8")])
+def test_fdct_unproven_units_listed_in_batches(oracle, q, fix_grid):
+    """K1 appends every unit its fast path cannot prove to one of 32 device
+    lists (unit ua to list ua % 32, one atomic counter per list) and
+    k_fdct_fix transforms the listed units in the reference's order
+    (k_transform.hip).  A K1 grid of 1 % of the resident workgroups
+    (MYYUV_K1_GRID_PCT) gives each wave hundreds of units of a noise batch,
+    a third or more of them unproven; with MYYUV_FIX_GRID=8 (q <= 75) the fix
+    kernel has 32 waves, one per list, so each walks its list's many entries
+    grid-stride.  Every frame must equal the oracle's."""
     import myyuv_hip
     import synth
 
-    old = os.environ.get("MYYUV_K1_GRID_PCT")
-    os.environ["MYYUV_K1_GRID_PCT"] = "1"
+    env = {"MYYUV_K1_GRID_PCT": "1", "MYYUV_FIX_GRID": fix_grid}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is not None:
+            os.environ[k] = v
     try:
         c = myyuv_hip.Codec(0)
     finally:
-        if old is None:
-            del os.environ["MYYUV_K1_GRID_PCT"]
-        else:
-            os.environ["MYYUV_K1_GRID_PCT"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     try:
         w, h = 2048, 1024  # 12,288 units over ~80 waves
         frames = [synth.noise_frame(w, h, seed=s).tobytes() for s in range(3)]

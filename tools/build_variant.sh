@@ -13,6 +13,6 @@ for k in k_transform k_huff_encode k_huff_decode k_stream k_color; do
 done
 /opt/rocm/bin/hipcc $F -x hip -c $C/myyuv_hip.cpp -o $out/myyuv_hip.o & objs="$objs $out/myyuv_hip.o"
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -fgpu-rdc --hip-link -shared -o $out/libmyyuv_hip.so $objs
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -fgpu-rdc --hip-link -shared -mllvm -vectorize-slp=false -o $out/libmyyuv_hip.so $objs
 rm -f $out/*.o
 echo built $out/libmyyuv_hip.so

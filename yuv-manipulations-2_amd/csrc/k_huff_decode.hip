@@ -49,18 +49,6 @@ constexpr uint32_t kStageQuads = 384;
 // the value needs no select.
 constexpr uint32_t kZeroBit = kStageQuads * 128u;
 
-// parse_table reads the chunk's first 20 bytes into registers at once (1)
-// or every byte from LDS as the group walk reaches it (0)
-#ifndef MYYUV_K5_TABLE_REGS
-#define MYYUV_K5_TABLE_REGS 1
-#endif
-
-// diagnostic ablations (never the product; 4: the non-constant blocks'
-// transform replaced by a copy, stores kept): 1 = no symbol decode, 2 = no
-// table parse either, 3 = the fused decoder skips its transform
-#ifndef MYYUV_K5_EXP
-#define MYYUV_K5_EXP 0
-#endif
 #ifndef MYYUV_K5_GROUP
 #define MYYUV_K5_GROUP 2  // positions per "any lane left" test (1 / 2 / 4 / 8: 132.4 / 128.2 / 129.0 / 135.1 us per launch, tools/runs/r3n.sh)
 #endif
@@ -126,7 +114,6 @@ struct Table {
 template <class Chunk>
 __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T) {
   if (s < 3) return 12;
-#if MYYUV_K5_TABLE_REGS
   // the chunk's first 20 bytes in registers, loaded together (the group walk
   // below is a chain of dependent byte reads: from registers, not one LDS
   // round trip per group; a table of at most 8 symbols ends within them)
@@ -141,9 +128,6 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T)
     }
     return c.byte(i);
   };
-#else
-  auto byte_at = [&](uint32_t i) -> uint32_t { return c.byte(i); };
-#endif
   const uint32_t nbits = byte_at(0) | (byte_at(1) << 8);
   const uint32_t tb = byte_at(2);
   if (nbits > 512 || 3 + tb + (nbits + 7) / 8 > s) return 12;
@@ -430,16 +414,10 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
     const LdsChunk lc{reinterpret_cast<const uint32_t*>(stq), mine ? cpos + rel - aw : 0u};
     Table T;
     int pcode = 0;
-#if MYYUV_K5_EXP != 2
     if (mine) pcode = parse_table(lc, s, T);
-#endif
     const bool go = mine && pcode == 0;
     int dcode = 0;
-#if MYYUV_K5_EXP == 0
     const bool failed = decode_regular(lc, T, go && T.regular, nw);
-#else
-    const bool failed = false;
-#endif
     // tables the reference never writes, and failed messages (for the
     // reference's exact error code): the bit-serial path
     if (go && (!T.regular || failed)) {
@@ -551,15 +529,6 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
       nw[4 * c + 3] = v.w;
     }
   }
-#if MYYUV_K5_EXP == 3
-  {
-    uint32_t x = 0;
-#pragma unroll
-    for (int w = 0; w < 32; w++) x += nw[w] * (2u * w + 1u);
-    if (x == 0x9E3779B9u) frame[lane] = 1;  // (keeps the decode live)
-    return;
-  }
-#endif
   // ---- K6 on the group.  Blocks whose only nonzero coefficient is the DC
   // (53 % of the bench frame's blocks) decode to one constant pixel value:
   // with Z[0][0] = z the only nonzero coefficient, stage 1 leaves U[i][0] =
@@ -630,15 +599,7 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     }
     xf::wave_sync();
     uint2 w0, w1;
-#if MYYUV_K5_EXP == 4  // diagnostic: the unit's transform replaced by its image's first words (stores kept)
-    {
-      const uint32_t* tw = reinterpret_cast<const uint32_t*>(tile + b * xf::kTile);
-      w0 = make_uint2(tw[q], tw[4 + q]);
-      w1 = make_uint2(tw[8 + q], tw[12 + q]);
-    }
-#else
     xf::idct_rows(tile + b * xf::kTile, q, sq, w0, w1);
-#endif
     if (16u * u + b < nrest) {
       const uint32_t gl = D.g0 + s_blk[16u * u + b];  // the block of compacted position 16u + b
       const uint32_t off = xf::block_row_offset(U, gl - U.cum, 2u * q);

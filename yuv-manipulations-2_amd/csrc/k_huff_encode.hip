@@ -997,14 +997,9 @@ __device__ __forceinline__ int wave_max_ln(int v, uint32_t ln) {
   return v;
 }
 
-#ifndef MYYUV_K2_DC_LDS
-#define MYYUV_K2_DC_LDS 1  // single-class runs take the DC from LDS (kept at classification), not from HBM
-#endif
 struct WinScratch {
   uint16_t slot[kWinBlocks];  // sorted position -> window slot (tile << 8 | block)
-#if MYYUV_K2_DC_LDS
-  uint16_t dc[kWinBlocks];    // window slot -> its DC coefficient (word 0 of quad 0)
-#endif
+  uint16_t dc[kWinBlocks];    // window slot -> its DC coefficient's low 11 bits (from K1's block word)
   uint8_t msz[kWinBlocks], cls[kWinBlocks], rm[kWinBlocks];
   uint32_t cnt[kScanVals];    // per (key, sort slot): count, then exclusive position
   uint32_t gb[kWinTiles];     // batch-global index of tile k's block 0
@@ -1089,9 +1084,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     const uint32_t cls = tid < nlk[k] ? (bi >> 15) & 7u : kClassDead;
     const uint32_t m = (bi >> 8) & 127u, rm = bi & 0xFFu;
     const uint32_t key = sort_key(cls, m);
-#if MYYUV_K2_DC_LDS
     sc.dc[(k << 8) | tid] = (uint16_t)(bi >> 18);  // the DC's low 11 bits (build_single_dc uses those)
-#endif
     uint32_t rk = 0;
 #pragma unroll
     for (uint32_t c = 0; c < kKeys; c++) {
@@ -1173,11 +1166,8 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     // round trip per quad)
     if (wcls == kClassSingle) {
       // one symbol: the DC coefficient (word 0 of quad 0), or 0
-#if MYYUV_K2_DC_LDS
+      // (single-class runs take the DC from LDS, kept at classification, not from HBM)
       const uint32_t dc = live ? (uint32_t)sc.dc[sl] : 0u;
-#else
-      const uint32_t dc = (live && (mrm & 1u)) ? reinterpret_cast<const uint32_t*>(coef)[coef_quad(mg, 0) * 4u] : 0u;
-#endif
       if (live) {
         build_single_dc((int)(int16_t)dc, S);
         ok = true;

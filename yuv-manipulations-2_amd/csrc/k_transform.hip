@@ -68,17 +68,6 @@
 #include "codec_common.hpp"
 #include "xform_common.hpp"
 
-#ifndef MYYUV_EXP
-#define MYYUV_EXP 0  // diagnostic ablations (tools/kab.sh builds); 0 = the product
-#endif
-#ifndef MYYUV_K1_PRIO
-#define MYYUV_K1_PRIO 0  // s_setprio level of K1's waves (tuning builds)
-#endif
-#ifdef MYYUV_XF_OCC  // register budget for MYYUV_XF_OCC waves per SIMD (tuning builds)
-#define MYYUV_XF_ATTR __attribute__((amdgpu_waves_per_eu(MYYUV_XF_OCC, MYYUV_XF_OCC)))
-#else
-#define MYYUV_XF_ATTR
-#endif
 // K1: 8 waves per SIMD (its LDS allows 8 workgroups per CU); the compiler
 // otherwise settles at 69 VGPRs (7 waves) with the block-info computation
 #ifndef MYYUV_K1_OCC
@@ -93,9 +82,6 @@ using namespace xf;
 // K1: u8 planes -> int16 coefficients (natural order, quad layout).
 // DCT.cpp:297-306 (gather, x - 128), :269-277 (applyDCTBlock).
 typedef unsigned short k1_us2 __attribute__((ext_vector_type(2)));
-#ifndef MYYUV_K1_PKMUL
-#define MYYUV_K1_PKMUL 1
-#endif
 
 // Rows 2q, 2q+1 of lane (b, q)'s block (coefficient quads 2q, 2q+1), the
 // block's row mask (bit c: row c has a nonzero coefficient, from the block's
@@ -113,12 +99,6 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
   uint4 lo, hi;
   uint32_t rm;
   pack_quads(c, q, lo, hi, rm);
-#if MYYUV_EXP == 2
-  if ((lo.x ^ hi.y ^ lo.z ^ hi.w ^ rm) == 0x7f3e5a11u) {  // never (keeps the transform live)
-    *dlo = lo;
-    *dhi = hi;
-  }
-#else
   // nonzero count and msz of the lane's natural pairs 8q .. 8q+7 (lo: row
   // 2q, hi: row 2q+1) in packed 16-bit arithmetic, as K2's block_class_msz:
   // flag = min(v, 1) per half, count += flag, max of (0 - flag) & (index + 1)
@@ -131,13 +111,9 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
     uint32_t fu, m16;
     asm("v_pk_min_u16 %0, %1, %2" : "=v"(fu) : "v"(wv[i]), "s"(0x00010001u));
     cnt += __builtin_bit_cast(k1_us2, fu);
-#if MYYUV_K1_PKMUL  // flag * (index + 1): the indices are VGPRs here, so the packed multiply takes them
+    // flag * (index + 1): the indices are VGPRs here, so the packed multiply takes them
     asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m16) : "v"(fu), "v"(zv[i]));
     mx = __builtin_elementwise_max(mx, __builtin_bit_cast(k1_us2, m16));
-#else
-    asm("v_pk_sub_u16 %0, 0, %1" : "=v"(m16) : "v"(fu));
-    mx = __builtin_elementwise_max(mx, __builtin_bit_cast(k1_us2, m16 & zv[i]));
-#endif
   }
   // the block's four lanes: counts add, msz is the maximum (one shuffle per
   // step carries both)
@@ -157,7 +133,6 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
   *(live ? binfo + g : reinterpret_cast<uint32_t*>(sink + 132) + lane) = binfo_word(rm, msz, class_of(nnz, msz), dc);
   *(nzl ? dlo : sink + lane) = lo;
   *(nzh ? dhi : sink + 64 + lane) = hi;
-#endif
 }
 
 // The zig-zag pair table in LDS (kZzPairs; before the tables' barrier)
@@ -175,9 +150,6 @@ __device__ __forceinline__ void stage_zz(uint4* szz) {
 // the units: 47k atomics per 8192x8192 frame, K1 83 -> 215 us); a per-wave
 // register list flushed 64 at a time fixed that but cost K1 4 % at q50
 // (profiles/r4r_*).
-#ifndef MYYUV_FIX_SPREAD
-#define MYYUV_FIX_SPREAD 1  // (0, A/B builds only: every unit in list 0)
-#endif
 
 __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t* __restrict__ frame, FrameGeom G,
                                                    const QTables* __restrict__ qt,
@@ -185,10 +157,6 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
                                                    uint32_t* __restrict__ binfo, uint4* __restrict__ sink,
                                                    uint32_t* __restrict__ k2ctl, uint32_t* __restrict__ fix,
                                                    uint32_t par) {
-#if MYYUV_K1_PRIO > 0
-  // wave issue priority over the other launch groups' kernels on the SIMD
-  __builtin_amdgcn_s_setprio(MYYUV_K1_PRIO);
-#endif
   // K2's overflow count for the launch that follows in the stream (nullptr: none)
   if (k2ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *k2ctl = 0u;
   __shared__ float tile[4][kXfUnit * kTile];
@@ -226,11 +194,7 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
     // (the last unit reloads itself: an unconditional load keeps the
     // in-order vmcnt accounting exact, so the loop top waits for these two
     // loads only, not for the stores behind them)
-#if MYYUV_EXP == 2  // diagnostic: compute only (pixels synthesised, stores below elided)
-    nx = make_uint4(ua * 2654435761u + lane, ua ^ 0x5bd1e995u, (ua + lane) * 40503u, ua * 69069u);
-#else
     nx = load_rows(frame, G, ua + stride < nall ? ua + stride : ua, b, q);
-#endif
     wave_sync();
 
     // stores of lanes past the plane's end go to the sink (no branch: see
@@ -238,24 +202,13 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
     uint4* dlo = live ? coef + coef_quad(g, 2 * q) : sink + lane;
     uint4* dhi = live ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
 
-#if MYYUV_EXP == 1  // diagnostic: memory only (same loads and stores, no transform)
-    {
-      const uint32_t h = (*reinterpret_cast<const uint32_t*>(img + 16u * q) ^
-                          *reinterpret_cast<const uint32_t*>(img + 16u * q + 8u)) & 0x00010001u;
-      const uint4 m = make_uint4(h, 0, 0, 0);  // small symbols: K2/K5 stay valid
-      wave_sync();
-      *dlo = m;
-      *dhi = m;
-    }
-    continue;
-#endif
     auto store = [&](const uint32_t (&c)[16]) {
       store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
     };
     uint32_t xr[4];
     fdct_load(img, q, xr);
     if (!fdct_fast(xr, tb, q, sqr, U.p, store) && lane == 0) {
-      const uint32_t c = MYYUV_FIX_SPREAD ? ua % kFixLists : 0u;
+      const uint32_t c = ua % kFixLists;
       // (a launch lists each unit at most once, so a count below the list's
       // capacity is guaranteed while k_fdct_fix resets the counts; the clamp
       // keeps a stale count, e.g. a diagnostic skip of the fix kernel, in bounds)
@@ -324,7 +277,7 @@ __global__ __launch_bounds__(64 * kFixWaves) void k_fdct_fix(const uint8_t* __re
 // K6: int16 coefficients (natural order, quad layout) -> u8 planes.
 // DCT.cpp:330-334 (dequant, squareMatrixMulT2, squareMatrixMul), :358-362
 // (roundf, +128, clamp).
-__global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4* __restrict__ coef,
+__global__ __launch_bounds__(256) void k_dequant_idct(const uint4* __restrict__ coef,
                                                      const uint8_t* __restrict__ rmask,
                                                      const uint4* __restrict__ zq, FrameGeom G,
                                                      const QTables* __restrict__ qt,
@@ -375,12 +328,6 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
       qk[2 * k + 1] = v.y;
     }
 
-#if MYYUV_EXP == 1  // diagnostic: memory only
-    uint32_t m = bits(qk[q]);
-#pragma unroll
-    for (int k = 0; k < 8; k++) m ^= zc[k];
-    const uint2 w0 = make_uint2(m, m + 1), w1 = make_uint2(m + 2, m + 3);
-#else
     // ---- dequantise (DCT.cpp:331) and stage 1: U[i][j] = sum_k D[k][i] * Z[k][j],
     // j in {2q, 2q+1} (squareMatrixMulT2<8>(DCT, Z), DCT.cpp:256-266)
     // Quantised blocks are sparse: a coefficient row k that is zero in all 16
@@ -443,7 +390,6 @@ __global__ __launch_bounds__(256) MYYUV_XF_ATTR void k_dequant_idct(const uint4*
                                 __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[15], px[13], 0x0c0c0400u),
                                                       __builtin_amdgcn_perm(px[11], px[9], 0x0c0c0400u),
                                                       0x05040100u));
-#endif
     // ---- pixel rows 2q, 2q+1 of the block out (8 B each; lanes past the
     // plane's end write the sink)
     {

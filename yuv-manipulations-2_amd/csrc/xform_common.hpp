@@ -38,35 +38,14 @@ __device__ __forceinline__ void wave_sync() {
 // Exchanges inside a block's four lanes (a DPP quad: lanes 4b .. 4b+3).  The
 // callers run with the whole wave active (K1's loop, k_fdct_fix's, the fused
 // encoder's phase 1: every branch around them is wave-uniform), so every
-// source lane is active; MYYUV_QUAD_DPP 0 uses ds_bpermute instead.
-#ifndef MYYUV_QUAD_DPP
-#define MYYUV_QUAD_DPP 1
-#endif
+// source lane is active.
 template <int kCtrl>  // quad_perm control
 __device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kCtrl, 0xF, 0xF, false);
 }
-__device__ __forceinline__ uint32_t quad_xor1(uint32_t v) {
-#if MYYUV_QUAD_DPP
-  return quad_perm<0xB1>(v);  // [1, 0, 3, 2]
-#else
-  return (uint32_t)__shfl_xor((int)v, 1, 64);
-#endif
-}
-__device__ __forceinline__ uint32_t quad_xor2(uint32_t v) {
-#if MYYUV_QUAD_DPP
-  return quad_perm<0x4E>(v);  // [2, 3, 0, 1]
-#else
-  return (uint32_t)__shfl_xor((int)v, 2, 64);
-#endif
-}
-__device__ __forceinline__ uint32_t quad_lane0(uint32_t v) {
-#if MYYUV_QUAD_DPP
-  return quad_perm<0x00>(v);  // [0, 0, 0, 0]
-#else
-  return (uint32_t)__shfl((int)v, (int)((threadIdx.x & 63u) & ~3u), 64);
-#endif
-}
+__device__ __forceinline__ uint32_t quad_xor1(uint32_t v) { return quad_perm<0xB1>(v); }   // [1, 0, 3, 2]
+__device__ __forceinline__ uint32_t quad_xor2(uint32_t v) { return quad_perm<0x4E>(v); }   // [2, 3, 0, 1]
+__device__ __forceinline__ uint32_t quad_lane0(uint32_t v) { return quad_perm<0x00>(v); }  // [0, 0, 0, 0]
 
 // Keeps 16 accumulators' updates in round-robin order (the scheduler would
 // otherwise serialise them chain by chain to save registers).
