@@ -484,6 +484,23 @@ __global__ __launch_bounds__(64, MYYUV_K5S_WAVES) void k_huff_decode(const uint8
   }
 }
 
+#ifdef MYYUV_STAMPS
+// diagnostic build only (-DMYYUV_STAMPS): the fused decoder's wave cycles
+// per phase, per wave (plain stores at the wave's end; contended atomics
+// would distort the timing): g_dec_wstamps[wave][8] = [4] decode (setup,
+// staging, table parse, symbol loop), [5] the DC blocks and the transform,
+// [7] = 1 for a wave that ran (myyuv_debug_dec_stamps, tools/dec_phase.py)
+__device__ uint32_t g_dec_wstamps[65536 * 8];
+#define DSTAMP(k)                                                \
+  do {                                                           \
+    __builtin_amdgcn_sched_barrier(0);                           \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();  \
+    __builtin_amdgcn_sched_barrier(0);                           \
+    _dacc[k] += (uint32_t)(_t - _dprev);                         \
+    _dprev = _t;                                                 \
+  } while (0)
+#endif
+
 // Fused decoder (K5 + K6; MYYUV_DECODER=fused): the wave decodes its 64-block
 // group as K5 does, then runs K6's transform on it as four 16-block units
 // straight from its registers: the unit's 16 decoding lanes write their
@@ -513,12 +530,19 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     sq[lane] = qt->q[p][lane];  // (ordered before idct_rows by decode_group's barriers)
   }
   if (desc[blockIdx.y].bad) return;
+#ifdef MYYUV_STAMPS
+  unsigned long long _dprev = __builtin_amdgcn_s_memtime();
+  uint32_t _dacc[8] = {0, 0, 0, 0, 0, 0, 1, 1};
+#endif
   DecodeGroup D;
   uint32_t nw[32];
 #pragma unroll
   for (int w = 0; w < 32; w++) nw[w] = 0;
   bool direct;
   decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw, direct);
+#ifdef MYYUV_STAMPS
+  DSTAMP(4);
+#endif
   if (D.live && direct) {  // decode_general wrote the block to coef (a table the reference never writes)
 #pragma unroll
     for (int c = 0; c < 8; c++) {
@@ -608,6 +632,11 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     }
     xf::wave_sync();  // the next unit rewrites the tile
   }
+#ifdef MYYUV_STAMPS
+  DSTAMP(5);
+  const uint32_t wid = blockIdx.y * gridDim.x + blockIdx.x;
+  if (lane < 8 && wid < 65536) g_dec_wstamps[wid * 8 + lane] = _dacc[lane];
+#endif
 }
 
 }  // namespace myyuv_gpu

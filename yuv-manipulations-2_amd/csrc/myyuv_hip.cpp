@@ -64,6 +64,7 @@ __global__ void k_bmp_to_iyuv(const uint8_t*, uint32_t, uint32_t, uint32_t, uint
 extern __device__ unsigned long long g_k2_stamps[40];
 extern __device__ uint32_t g_k2_wstamps[65536 * 8];
 extern __device__ uint32_t g_k2_fstamps[8192 * 8];
+extern __device__ uint32_t g_dec_wstamps[65536 * 8];
 #endif
 }  // namespace myyuv_gpu
 
@@ -1030,6 +1031,22 @@ int myyuv_debug_k2_wstamps(uint32_t* out, uint32_t n) {
 #ifdef MYYUV_STAMPS
   if (n > 65536) n = 65536;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_wstamps), (size_t)n * 32) == hipSuccess ? 0 : MYYUV_E_HIP;
+#else
+  (void)out;
+  (void)n;
+  return MYYUV_E_ARG;
+#endif
+}
+
+// Diagnostic builds (-DMYYUV_STAMPS): the fused decoder's per-phase wave
+// cycles of the last launch, n waves x 8 words (k_huff_decode.hip
+// g_dec_wstamps; word 7 = 1 for a wave that ran), then zeroed.
+int myyuv_debug_dec_stamps(uint32_t* out, uint32_t n) {
+#ifdef MYYUV_STAMPS
+  if (n > 65536) n = 65536;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec_wstamps), (size_t)n * 32) != hipSuccess) return MYYUV_E_HIP;
+  std::vector<uint32_t> zero((size_t)n * 8, 0u);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dec_wstamps), zero.data(), (size_t)n * 32) == hipSuccess ? 0 : MYYUV_E_HIP;
 #else
   (void)out;
   (void)n;
