@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: the fused decoder's wave cycles per phase (decode, then the
-DC blocks and the transform; stamp build,
+DC blocks and the transform, split into setup, staging, table parse and
+symbol loop; stamp build,
 `tools/build_variant.sh stamps -DMYYUV_STAMPS`; k_huff_decode.hip
 g_dec_stamps), one 24-frame launch group of the bench frame decoded alone:
   MYYUV_HIP_LIB=build_var/stamps/libmyyuv_hip.so python3 tools/dec_phase.py [frames]"""
@@ -47,9 +48,9 @@ rc = L.myyuv_debug_dec_stamps(buf, NW)
 import numpy as np  # noqa: E402
 a = np.frombuffer(buf, np.uint32).reshape(NW, 8).astype(np.float64)
 a = a[a[:, 7] > 0]
-names = {4: "decode", 5: "DC + transform"}
+names = {0: "setup+scan", 1: "staging", 2: "table parse", 3: "symbol loop", 4: "(rest of decode)", 5: "DC + transform"}
 tot = a[:, :6].sum()
-print(f"rc={rc} kernel {kms / kn * 1e3:.1f} us per {B}-frame launch; waves stamped {len(a)}")
+print(f"rc={rc} kernel {kms / kn * 1e3:.1f} us per {B}-frame launch; waves stamped {len(a)}, rounds/wave {a[:, 6].mean():.2f}")
 for i, nm in names.items():
     print(f"  {nm:16s} {a[:, i].mean():9.0f} cycles/wave (p90 {np.percentile(a[:, i], 90):8.0f})  {a[:, i].sum() / tot:6.1%}")
 print(f"  total            {a[:, :6].sum(1).mean():9.0f} cycles/wave (p90 {np.percentile(a[:, :6].sum(1), 90):8.0f})")

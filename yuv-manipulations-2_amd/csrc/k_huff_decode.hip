@@ -296,6 +296,35 @@ __device__ __forceinline__ int decode_general(const LdsChunk c, const Table T, u
 
 }  // namespace
 
+#ifdef MYYUV_STAMPS
+// diagnostic build only (-DMYYUV_STAMPS): the fused decoder's wave cycles
+// per phase, per wave (plain stores at the wave's end; contended atomics
+// would distort the timing): g_dec_wstamps[wave][8] = [0] setup (sizes,
+// scan, offsets), [1] staging, [2] table parse, [3] symbol loop, [5] the DC
+// blocks and the transform, [6] rounds, [7] = 1 for a wave that ran
+// (myyuv_debug_dec_stamps, tools/dec_phase.py)
+__device__ uint32_t g_dec_wstamps[65536 * 8];
+struct DStamps {
+  unsigned long long prev;
+  uint32_t acc[8];
+};
+#define DSTAMP(k)                                                \
+  do {                                                           \
+    if (ds != nullptr) {                                         \
+      __builtin_amdgcn_sched_barrier(0);                         \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+      __builtin_amdgcn_sched_barrier(0);                         \
+      ds->acc[k] += (uint32_t)(_t - ds->prev);                   \
+      ds->prev = _t;                                             \
+    }                                                            \
+  } while (0)
+#else
+struct DStamps {};
+#define DSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 // K5's decode of one wave's 64-block group (blockIdx.x) of frame blockIdx.y:
 // the natural-order words of each lane's block in nw (or, for a table that is
 // not "regular", written to coef by decode_general: *direct).  Returns false
@@ -311,7 +340,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
                                              const uint32_t* __restrict__ tile_pre, const FrameGeom& G,
                                              uint32_t tiles_p0, uint32_t tiles_p1, uint4* __restrict__ coef,
                                              unsigned long long* __restrict__ err, uint4* stq, DecodeGroup& D,
-                                             uint32_t (&nw)[32], bool& direct) {
+                                             uint32_t (&nw)[32], bool& direct, DStamps* ds = nullptr) {
   // frame blockIdx.y of the batch: its stream slot, descriptor and scan;
   // coefficients at batch-global block gbase + g
   const uint32_t f = blockIdx.y;
@@ -370,7 +399,11 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   // needs one round per wave.
   const uint4 zero = make_uint4(0, 0, 0, 0);
   uint64_t pending = __ballot(ok);
+  DSTAMP(0);
   while (pending) {
+#ifdef MYYUV_STAMPS
+    if (ds != nullptr) ds->acc[6] += 1;
+#endif
     const int lo = __ffsll((long long)pending) - 1;
     const uint32_t A = cpos + __shfl(rel, lo, 64);
     const uint32_t aw = A & ~15u;
@@ -409,6 +442,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
       stq[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     __syncthreads();
+    DSTAMP(1);
 
     const bool mine = ((pending >> lane) & 1) && cpos + rel + s <= wend;
     const LdsChunk lc{reinterpret_cast<const uint32_t*>(stq), mine ? cpos + rel - aw : 0u};
@@ -417,6 +451,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
     if (mine) pcode = parse_table(lc, s, T);
     const bool go = mine && pcode == 0;
     int dcode = 0;
+    DSTAMP(2);
     const bool failed = decode_regular(lc, T, go && T.regular, nw);
     // tables the reference never writes, and failed messages (for the
     // reference's exact error code): the bit-serial path
@@ -426,6 +461,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
     }
     if (mine) code = go ? dcode : pcode;
     pending &= ~__ballot(mine);
+    DSTAMP(3);
     __syncthreads();  // the next round overwrites the stage
   }
   if (ok && code) record_error(err, 2ull * (gbase + g) + 1, code);
@@ -484,23 +520,6 @@ __global__ __launch_bounds__(64, MYYUV_K5S_WAVES) void k_huff_decode(const uint8
   }
 }
 
-#ifdef MYYUV_STAMPS
-// diagnostic build only (-DMYYUV_STAMPS): the fused decoder's wave cycles
-// per phase, per wave (plain stores at the wave's end; contended atomics
-// would distort the timing): g_dec_wstamps[wave][8] = [4] decode (setup,
-// staging, table parse, symbol loop), [5] the DC blocks and the transform,
-// [7] = 1 for a wave that ran (myyuv_debug_dec_stamps, tools/dec_phase.py)
-__device__ uint32_t g_dec_wstamps[65536 * 8];
-#define DSTAMP(k)                                                \
-  do {                                                           \
-    __builtin_amdgcn_sched_barrier(0);                           \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();  \
-    __builtin_amdgcn_sched_barrier(0);                           \
-    _dacc[k] += (uint32_t)(_t - _dprev);                         \
-    _dprev = _t;                                                 \
-  } while (0)
-#endif
-
 // Fused decoder (K5 + K6; MYYUV_DECODER=fused): the wave decodes its 64-block
 // group as K5 does, then runs K6's transform on it as four 16-block units
 // straight from its registers: the unit's 16 decoding lanes write their
@@ -531,18 +550,21 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
   }
   if (desc[blockIdx.y].bad) return;
 #ifdef MYYUV_STAMPS
-  unsigned long long _dprev = __builtin_amdgcn_s_memtime();
-  uint32_t _dacc[8] = {0, 0, 0, 0, 0, 0, 1, 1};
+  DStamps dst;
+  DStamps* ds = &dst;
+  dst.prev = __builtin_amdgcn_s_memtime();
+#pragma unroll
+  for (int k = 0; k < 8; k++) dst.acc[k] = k == 7 ? 1u : 0u;
+#else
+  DStamps* ds = nullptr;
 #endif
   DecodeGroup D;
   uint32_t nw[32];
 #pragma unroll
   for (int w = 0; w < 32; w++) nw[w] = 0;
   bool direct;
-  decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw, direct);
-#ifdef MYYUV_STAMPS
+  decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw, direct, ds);
   DSTAMP(4);
-#endif
   if (D.live && direct) {  // decode_general wrote the block to coef (a table the reference never writes)
 #pragma unroll
     for (int c = 0; c < 8; c++) {
@@ -632,10 +654,12 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     }
     xf::wave_sync();  // the next unit rewrites the tile
   }
-#ifdef MYYUV_STAMPS
   DSTAMP(5);
+#ifdef MYYUV_STAMPS
   const uint32_t wid = blockIdx.y * gridDim.x + blockIdx.x;
-  if (lane < 8 && wid < 65536) g_dec_wstamps[wid * 8 + lane] = _dacc[lane];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if (lane == (uint32_t)k && wid < 65536) g_dec_wstamps[wid * 8 + k] = dst.acc[k];
 #endif
 }
 
