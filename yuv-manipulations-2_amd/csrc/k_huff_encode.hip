@@ -1132,9 +1132,6 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   const uint32_t nlive = sc.cnt[kDeadKey * kWinRuns];
   __syncthreads();
   const uint32_t nruns = (nlive + kWave - 1) / kWave;
-#if defined(MYYUV_K2_EXP) && MYYUV_K2_EXP == 1
-  if (nruns < 1000000u) return;  // diagnostic: classify + sort only
-#endif
   // ---- 3. the runs, heaviest first
   while (true) {
     uint32_t r = 0;
