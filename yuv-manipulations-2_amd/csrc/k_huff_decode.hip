@@ -81,6 +81,20 @@ __device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uin
   return local_off[g] + tile_pre[g / kScanTile];
 }
 
+// Inclusive sum over the wave's 64 lanes by DPP (rows of 16 by row_shr 1, 2,
+// 4, 8, then row_bcast 15 / 31 across rows; lanes whose source is out of
+// range add the old value 0).  Every lane must be active: under a partial
+// EXEC, inactive lanes pass nothing on (the DPP rule).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
 }
@@ -369,17 +383,43 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   const uint32_t cpos = desc->content_pos[p];
   const uint32_t csize = desc->content_size[p];
   const uint32_t E = cpos + min(end_scan - plane_pre, csize);
+  // Round 1 stages from the group's first chunk (lane 0's: g0 < g1, so lane
+  // 0 is live; when it is not ok, no lane is and no round runs).  Its
+  // position needs no size byte, so its loads go out together with the size
+  // bytes' (issued just before them: the VMEM counter drains in order, so
+  // the size bytes' wait covers them either way) instead of after the size
+  // scan: one dependent load round trip less before the table parse.
+  const uint32_t pre0 = scanned(local_off, tile_pre, g0) - plane_pre;
+  auto window = [&](uint32_t A, uint32_t& aw, uint32_t& wend, uint32_t& nq, uint32_t& nfull) {
+    aw = A & ~15u;
+    wend = aw + 16 * (kStageQuads - 1);
+    nq = E > aw ? (min(E, wend) - aw + 15) >> 4 : 0u;
+    nfull = limit >= aw ? min(nq, (limit - aw) >> 4) : 0u;  // quads below limit
+  };
+  // the first 256 quads straight into the stage (LDS-DMA: quad 64m + lane
+  // from instruction m), all in flight together and holding no registers.
+  // Unconditional, at clamped addresses: the quads they write at or past
+  // nfull are rewritten by stage() up to nq, and past nq nothing reads the
+  // stage
+  auto load4 = [&](uint32_t aw, uint32_t nfull) {
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const uint8_t* src = nfull > 0 ? in + aw + 16 * min(lane + 64u * m, nfull - 1) : in;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(stq + 64 * m),
+                                       16, 0, 0);
+    }
+  };
+  uint32_t aw, wend, nq, nfull;
+  window(cpos + pre0, aw, wend, nq, nfull);
+  load4(aw, nfull);
+  __builtin_amdgcn_sched_barrier(0);  // (all four issued before the size bytes' load)
   const uint32_t gl = live ? g : g1 - 1;
   const uint32_t s = in[desc->sizes_pos[p] + (gl - G.cum[p])];
   // the chunk's offset: the group's (k_scan_chain keeps group starts only)
   // plus the wave's exclusive scan of the sizes
-  uint32_t incl = live ? s : 0u;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
-  }
-  const uint32_t rel = scanned(local_off, tile_pre, g0) - plane_pre + incl - (live ? s : 0u);
+  // (by DPP, the whole wave active: six ds_bpermute round trips less)
+  const uint32_t incl = wave_incl_scan(live ? s : 0u);
+  const uint32_t rel = pre0 + incl - (live ? s : 0u);
 
   // plane-level check (DCT.cpp:21-33 reads past content_size otherwise):
   // the chunks must fit the declared content.
@@ -397,40 +437,15 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   // decode the lanes whose chunks are inside.  Chunks are consecutive and at
   // most 255 B, so every round retires at least one lane; a 4K frame at q=50
   // needs one round per wave.
-  const uint4 zero = make_uint4(0, 0, 0, 0);
   uint64_t pending = __ballot(ok);
   DSTAMP(0);
-  while (pending) {
-#ifdef MYYUV_STAMPS
-    if (ds != nullptr) ds->acc[6] += 1;
-#endif
-    const int lo = __ffsll((long long)pending) - 1;
-    const uint32_t A = cpos + __shfl(rel, lo, 64);
-    const uint32_t aw = A & ~15u;
-    const uint32_t wend = aw + 16 * (kStageQuads - 1);
-    const uint32_t nq = (min(E, wend) - aw + 15) >> 4;
-    const uint32_t nfull = limit >= aw ? min(nq, (limit - aw) >> 4) : 0;  // quads below limit
-    // the first 256 quads: loads at clamped addresses, all in flight before
-    // the first LDS write
-    uint4 r[4] = {zero, zero, zero, zero};
-    if (nfull > 0) {
-#pragma unroll
-      for (int m = 0; m < 4; m++) {
-        const uint32_t k = min(lane + 64u * m, nfull - 1);
-        r[m] = *reinterpret_cast<const uint4*>(in + aw + 16 * k);
-      }
-#pragma unroll
-      for (int m = 0; m < 4; m++)
-        asm volatile("" : "+v"(r[m].x), "+v"(r[m].y), "+v"(r[m].z), "+v"(r[m].w));
-    }
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-      const uint32_t k = lane + 64 * m;
-      if (k < nfull) stq[k] = r[m];
-    }
+  // the rest of one round's stage: the window past 256 quads, zeros at or
+  // past `limit` and the slack quad
+  auto stage = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // load4's LDS writes (before the zero quads)
     for (uint32_t k = lane + 256; k < nfull; k += 64)
       stq[k] = *reinterpret_cast<const uint4*>(in + aw + 16 * k);
-    for (uint32_t k = nfull + lane; k <= nq; k += 64) {  // at or past `limit`, and the slack quad
+    for (uint32_t k = nfull + lane; k <= nq; k += 64) {
       uint32_t v[4] = {0, 0, 0, 0};
       if (k < nq) {
 #pragma unroll
@@ -442,6 +457,12 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
       stq[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     __syncthreads();
+  };
+  if (pending) stage();
+  while (pending) {
+#ifdef MYYUV_STAMPS
+    if (ds != nullptr) ds->acc[6] += 1;
+#endif
     DSTAMP(1);
 
     const bool mine = ((pending >> lane) & 1) && cpos + rel + s <= wend;
@@ -462,7 +483,13 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
     if (mine) code = go ? dcode : pcode;
     pending &= ~__ballot(mine);
     DSTAMP(3);
-    __syncthreads();  // the next round overwrites the stage
+    if (pending) {  // the next round, from the lowest pending lane's chunk
+      __syncthreads();  // it overwrites the stage
+      const int lo = __ffsll((long long)pending) - 1;
+      window(cpos + __shfl(rel, lo, 64), aw, wend, nq, nfull);
+      load4(aw, nfull);
+      stage();
+    }
   }
   if (ok && code) record_error(err, 2ull * (gbase + g) + 1, code);
   D.f = f;

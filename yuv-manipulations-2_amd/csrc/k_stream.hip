@@ -161,6 +161,10 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
   // (one dependent round trip per tile measured 14 us per 4032x3008 frame,
   // 22 us per 8192x8192 one), and kept in registers for the prefix pass
   constexpr uint32_t kTsBatch = 8;
+  // tiles per thread kept in registers between the two passes (256 x 32 =
+  // 8,192 tiles: an 8192x8192 frame has 6,144); above, the second pass
+  // reloads its totals, a batch at a time
+  constexpr uint32_t kTsKeep = 32;
   __shared__ uint32_t s_w[4];
   __shared__ uint32_t s_carry;
   const uint32_t f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -172,18 +176,36 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
     const uint4 a = *reinterpret_cast<const uint4*>(w);
     return a.x + a.y + a.z + a.w + w[4];
   };
-  uint32_t v = 0, keep[kTsBatch];
-  for (uint32_t k0 = 0; k0 < per; k0 += kTsBatch) {
-    uint32_t x[kTsBatch];
+  // tiles k0 .. k0 + 7 of this thread: unconditional loads at clamped
+  // indices, so all eight are in flight together (a guarded load is a branch
+  // with its own wait)
+  auto batch = [&](uint32_t k0, uint32_t (&x)[kTsBatch]) {
 #pragma unroll
     for (uint32_t j = 0; j < kTsBatch; j++) {
       const uint32_t t = tid * per + k0 + j;
-      x[j] = (k0 + j < per && t < ntile) ? total(t) : 0u;
+      const uint32_t tv = total(min(t, ntile - 1));
+      x[j] = (k0 + j < per && t < ntile) ? tv : 0u;
     }
+  };
+  const bool kept = per <= kTsKeep;
+  uint32_t v = 0, keep[kTsKeep];
+  if (kept) {
 #pragma unroll
-    for (uint32_t j = 0; j < kTsBatch; j++) {
-      v += x[j];
-      keep[j] = x[j];  // (used when there is one batch: per <= kTsBatch)
+    for (uint32_t k0 = 0; k0 < kTsKeep; k0 += kTsBatch) {
+      uint32_t x[kTsBatch] = {};
+      if (k0 < per) batch(k0, x);
+#pragma unroll
+      for (uint32_t j = 0; j < kTsBatch; j++) {
+        v += x[j];
+        keep[k0 + j] = x[j];
+      }
+    }
+  } else {
+    for (uint32_t k0 = 0; k0 < per; k0 += kTsBatch) {
+      uint32_t x[kTsBatch];
+      batch(k0, x);
+#pragma unroll
+      for (uint32_t j = 0; j < kTsBatch; j++) v += x[j];
     }
   }
   const uint32_t incl = wave_inclusive_scan(v);
@@ -196,9 +218,9 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
     tot += s_w[k];
   }
   pre += incl - v;
-  if (per <= kTsBatch) {
+  if (kept) {
 #pragma unroll
-    for (uint32_t j = 0; j < kTsBatch; j++) {
+    for (uint32_t j = 0; j < kTsKeep; j++) {
       const uint32_t t = tid * per + j;
       if (j < per && t < ntile) {
         info[(size_t)t * kTInfoWords + kTInfoPrefix] = pre;
@@ -206,12 +228,16 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
       }
     }
   } else {
-    for (uint32_t k = 0; k < per; k++) {
-      const uint32_t t = tid * per + k;
-      if (t < ntile) {
-        const uint32_t x = total(t);
-        info[(size_t)t * kTInfoWords + kTInfoPrefix] = pre;
-        pre += x;
+    for (uint32_t k0 = 0; k0 < per; k0 += kTsBatch) {
+      uint32_t x[kTsBatch];
+      batch(k0, x);
+#pragma unroll
+      for (uint32_t j = 0; j < kTsBatch; j++) {
+        const uint32_t t = tid * per + k0 + j;
+        if (k0 + j < per && t < ntile) {
+          info[(size_t)t * kTInfoWords + kTInfoPrefix] = pre;
+          pre += x[j];
+        }
       }
     }
   }
