@@ -358,30 +358,46 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   // frame blockIdx.y of the batch: its stream slot, descriptor and scan;
   // coefficients at batch-global block gbase + g
   const uint32_t f = blockIdx.y;
-  const uint32_t gbase = f * G.cum[3];
-  const uint32_t ntiles = (G.cum[3] + kScanTile - 1) / kScanTile;
+  const uint32_t nblk = G.cum[3];
+  const uint32_t gbase = f * nblk;
+  const uint32_t ntiles = (nblk + kScanTile - 1) / kScanTile;
   in += (size_t)f * cap;
   desc += f;
   local_off += gbase;
   tile_pre += (size_t)f * (ntiles + 1);
-  if (desc->bad) return false;
   const int lane = threadIdx.x;
   const uint32_t t = blockIdx.x;
   const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
-  const uint32_t tile_in_plane = t - (p == 0 ? 0 : (p == 1 ? tiles_p0 : tiles_p0 + tiles_p1));
-  const uint32_t g0 = G.cum[p] + tile_in_plane * kWave;
-  const uint32_t g1 = min(g0 + kWave, G.cum[p + 1]);
+  // the plane's fields by static index (a dynamic index into the kernel
+  // argument G, or into the descriptor once loaded, is a scalar load: one
+  // more dependent round trip)
+  auto sel3 = [p](uint32_t a0, uint32_t a1, uint32_t a2) { return p == 0 ? a0 : (p == 1 ? a1 : a2); };
+  const uint32_t cum_p = sel3(G.cum[0], G.cum[1], G.cum[2]), cum_p1 = sel3(G.cum[1], G.cum[2], G.cum[3]);
+  const uint32_t tile_in_plane = t - sel3(0u, tiles_p0, tiles_p0 + tiles_p1);
+  const uint32_t g0 = cum_p + tile_in_plane * kWave;
+  const uint32_t g1 = min(g0 + kWave, cum_p1);
   const uint32_t g = g0 + lane;
   const bool live = g < g1;
-  const uint32_t limit = min(in_size[f], cap);
-  const uint32_t nblk = G.cum[3];
-
-  // end of the wave's chunk range from the scan alone (rel(nblk) = the total)
-  const uint32_t plane_pre = scanned(local_off, tile_pre, G.cum[p]);
-  const uint32_t end_scan = g1 == nblk ? tile_pre[(nblk + kScanTile - 1) / kScanTile]
-                                       : scanned(local_off, tile_pre, g1);
-  const uint32_t cpos = desc->content_pos[p];
-  const uint32_t csize = desc->content_size[p];
+  // every scalar of the setup in one round trip: the descriptor, the payload
+  // size, the scan at the plane's start and the group's ends.  No branch on
+  // `bad` in front of them (it would hold the rest back by a round trip): a
+  // bad frame decodes nothing (no lane is ok) and returns false below.
+  const StreamDesc dsc = *desc;
+  const uint32_t isz = in_size[f];
+  const uint32_t g1c = min(g1, nblk - 1);
+  const uint32_t lo_p = local_off[cum_p], tp_p = tile_pre[cum_p / kScanTile];
+  const uint32_t lo_0 = local_off[g0], tp_0 = tile_pre[g0 / kScanTile];
+  const uint32_t lo_1 = local_off[g1c], tp_1 = tile_pre[g1c / kScanTile];
+  const uint32_t stot = tile_pre[ntiles];  // rel(nblk) = the total
+  __builtin_amdgcn_sched_barrier(0);  // (all issued before the first use waits)
+  const uint32_t plane_pre = lo_p + tp_p, s0 = lo_0 + tp_0, s1 = lo_1 + tp_1;
+  const bool bad = dsc.bad != 0;
+  const uint32_t limit = bad ? 0u : min(isz, cap);
+  // end of the wave's chunk range from the scan alone
+  const uint32_t end_scan = g1 == nblk ? stot : s1;
+  const uint32_t cpos = sel3(dsc.content_pos[0], dsc.content_pos[1], dsc.content_pos[2]);
+  const uint32_t csize = sel3(dsc.content_size[0], dsc.content_size[1], dsc.content_size[2]);
+  const uint32_t spos = sel3(dsc.sizes_pos[0], dsc.sizes_pos[1], dsc.sizes_pos[2]);
   const uint32_t E = cpos + min(end_scan - plane_pre, csize);
   // Round 1 stages from the group's first chunk (lane 0's: g0 < g1, so lane
   // 0 is live; when it is not ok, no lane is and no round runs).  Its
@@ -389,7 +405,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   // bytes' (issued just before them: the VMEM counter drains in order, so
   // the size bytes' wait covers them either way) instead of after the size
   // scan: one dependent load round trip less before the table parse.
-  const uint32_t pre0 = scanned(local_off, tile_pre, g0) - plane_pre;
+  const uint32_t pre0 = s0 - plane_pre;
   auto window = [&](uint32_t A, uint32_t& aw, uint32_t& wend, uint32_t& nq, uint32_t& nfull) {
     aw = A & ~15u;
     wend = aw + 16 * (kStageQuads - 1);
@@ -414,7 +430,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   load4(aw, nfull);
   __builtin_amdgcn_sched_barrier(0);  // (all four issued before the size bytes' load)
   const uint32_t gl = live ? g : g1 - 1;
-  const uint32_t s = in[desc->sizes_pos[p] + (gl - G.cum[p])];
+  const uint32_t s = in[bad ? 0u : spos + (gl - cum_p)];
   // the chunk's offset: the group's (k_scan_chain keeps group starts only)
   // plus the wave's exclusive scan of the sizes
   // (by DPP, the whole wave active: six ds_bpermute round trips less)
@@ -423,9 +439,9 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
 
   // plane-level check (DCT.cpp:21-33 reads past content_size otherwise):
   // the chunks must fit the declared content.
-  bool ok = live;
-  if (live && rel + s > csize) {
-    record_error(err, 2ull * (gbase + G.cum[p]), 9 /* MYYUV_E_PLANE_CONTENT */);
+  bool ok = live && !bad;
+  if (ok && rel + s > csize) {
+    record_error(err, 2ull * (gbase + cum_p), 9 /* MYYUV_E_PLANE_CONTENT */);
     ok = false;
   }
 
@@ -491,6 +507,10 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
       stage();
     }
   }
+  // every LDS-DMA load has landed before the stage is reused or the wave
+  // ends, whether or not a round ran (no lane ok: round 1's loads were still
+  // issued)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (ok && code) record_error(err, 2ull * (gbase + g) + 1, code);
   D.f = f;
   D.gbase = gbase;
@@ -499,7 +519,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   D.g = g;
   D.p = p;
   D.live = live;
-  return true;
+  return !bad;
 }
 
 __global__ __launch_bounds__(64, MYYUV_K5S_WAVES) void k_huff_decode(const uint8_t* __restrict__ in,
@@ -515,19 +535,16 @@ __global__ __launch_bounds__(64, MYYUV_K5S_WAVES) void k_huff_decode(const uint8
                                                    unsigned long long* __restrict__ err) {
   __shared__ uint4 stq[kStageQuads + 1];
   if (threadIdx.x == 0) stq[kStageQuads] = make_uint4(0u, 0u, 0u, 0u);  // (ordered by decode_group's barrier)
-  if (desc[blockIdx.y].bad) return;
   DecodeGroup D;
   uint32_t nw[32];
 #pragma unroll
   for (int w = 0; w < 32; w++) nw[w] = 0;
   bool direct;
-  decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw, direct);
-  const uint32_t gbase = blockIdx.y * G.cum[3];
-  const uint32_t t = blockIdx.x;
-  const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
-  const uint32_t tile_in_plane = t - (p == 0 ? 0 : (p == 1 ? tiles_p0 : tiles_p0 + tiles_p1));
-  const uint32_t g = G.cum[p] + tile_in_plane * kWave + threadIdx.x;
-  const bool live = g < min(G.cum[p] + tile_in_plane * kWave + kWave, G.cum[p + 1]);
+  if (!decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw,
+                    direct))
+    return;  // the frame's stream header is bad (k_scan_chain recorded it)
+  const uint32_t gbase = D.gbase, g = D.g;
+  const bool live = D.live;
   // ---- natural-order words to the quad layout (1 KiB contiguous per store)
   // Only the nonzero rows are stored; bit c of the block's row mask says
   // whether row c holds a nonzero coefficient, and K6 reads just those.
@@ -571,11 +588,13 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
   const uint32_t lane = threadIdx.x;
   if (lane == 0) stq[kStageQuads] = make_uint4(0u, 0u, 0u, 0u);  // (ordered by decode_group's barrier)
   {
+    // the plane's Q table by LDS-DMA (no register, no wait here; landed by
+    // decode_group's final vmcnt wait, before idct_rows)
     const uint32_t t = blockIdx.x;
     const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
-    sq[lane] = qt->q[p][lane];  // (ordered before idct_rows by decode_group's barriers)
+    __builtin_amdgcn_global_load_lds((const void*)&qt->q[p][lane], (__attribute__((address_space(3))) void*)sq, 4,
+                                     0, 0);
   }
-  if (desc[blockIdx.y].bad) return;
 #ifdef MYYUV_STAMPS
   DStamps dst;
   DStamps* ds = &dst;
@@ -590,7 +609,9 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
 #pragma unroll
   for (int w = 0; w < 32; w++) nw[w] = 0;
   bool direct;
-  decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw, direct, ds);
+  if (!decode_group(in, in_size, cap, desc, local_off, tile_pre, G, tiles_p0, tiles_p1, coef, err, stq, D, nw,
+                    direct, ds))
+    return;  // the frame's stream header is bad (k_scan_chain recorded it)
   DSTAMP(4);
   if (D.live && direct) {  // decode_general wrote the block to coef (a table the reference never writes)
 #pragma unroll
