@@ -33,6 +33,25 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
   return v;
 }
 
+// The same by DPP (rows of 16 by row_shr 1, 2, 4, 8, then row_bcast 15 / 31
+// across rows): no LDS round trip.  Every lane of the wave must be active
+// (under a partial EXEC, inactive lanes pass nothing on).
+__device__ __forceinline__ uint32_t wave_inclusive_scan_dpp(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
+// Lane i + 1's value in lane i (DPP wave_shl:1; lane 63 gets 0), every lane
+// active.
+__device__ __forceinline__ uint32_t wave_next_lane(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
+}
+
 __device__ __forceinline__ void record_error(unsigned long long* err, uint64_t key, int code) {
   atomicMin(err, (unsigned long long)((key << 8) | (uint64_t)code));
 }
@@ -284,29 +303,54 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
                                                     uint8_t* __restrict__ out, uint32_t cap) {
   __shared__ uint32_t s_wt[4], s_hdr[4];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t ntile = G.tcum[3];
+  // the kernel arguments this workgroup uses, consumed at once (the compiler
+  // would otherwise load them in three dependent batches, each where it is
+  // first used)
+  uint32_t ntile = G.tcum[3], nframes = G.nframes, tc1 = G.tcum[1], tc2 = G.tcum[2];
+  uint32_t c1 = G.cum[1], c2 = G.cum[2], c3 = G.cum[3];
+  asm volatile("" : "+s"(ntile), "+s"(nframes), "+s"(tc1), "+s"(tc2), "+s"(c1), "+s"(c2), "+s"(c3), "+s"(cap),
+               "+s"(stage), "+s"(oslots));
   // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and
   // b + 8 share one L2), and a K2 window's kWinTiles tiles read interleaved
   // pieces of the same stage lines, so they go to one XCD: workgroup L takes
   // batch tile kWinTiles * (8 * (L / (8 kWinTiles)) + L % 8) + (L / 8) %
   // kWinTiles (a bijection on the grid, a multiple of 8 * kWinTiles)
   const uint32_t L = blockIdx.x, slot = L >> 3;
-  const uint32_t T = kWinTiles * ((slot / kWinTiles) * 8u + (L & 7u)) + slot % kWinTiles;
-  if (T >= ntile * G.nframes) return;
+  const uint32_t T0 = kWinTiles * ((slot / kWinTiles) * 8u + (L & 7u)) + slot % kWinTiles;
+  // a surplus workgroup (the grid is a multiple of 8 * kWinTiles) runs the
+  // first round trip on the last tile and returns after it: no branch ahead
+  // of the kernel-argument and first loads
+  const bool surplus = T0 >= ntile * nframes;
+  const uint32_t T = surplus ? ntile * nframes - 1 : T0;
   const uint32_t f = T / ntile, t = T - f * ntile;
-  const int p = tile_plane(G, t);
-  const uint32_t g0 = tile_first(G, p, t);
-  const uint32_t nloc = min(kK2Group, G.cum[p + 1] - g0);
-  const uint32_t gb = f * G.cum[3] + g0;
+  const int p = t >= tc1 ? (t >= tc2 ? 2 : 1) : 0;  // tile_plane
+  // the plane's fields by static index (a dynamic index into the kernel
+  // argument G is a scalar load: one more dependent round trip)
+  auto sel3 = [p](uint32_t a0, uint32_t a1, uint32_t a2) { return p == 0 ? a0 : (p == 1 ? a1 : a2); };
+  const uint32_t cum_p = sel3(0u, c1, c2), cum_p1 = sel3(c1, c2, c3);  // (cum[0] = tcum[0] = 0)
+  const uint32_t tcum_p = sel3(0u, tc1, tc2);
+  const uint32_t g0 = cum_p + (t - tcum_p) * kK2Group;
+  const uint32_t nloc = min(kK2Group, cum_p1 - g0);
+  const uint32_t gb = f * c3 + g0;
   out += (size_t)f * cap;
-  const uint32_t x = tinfo[(size_t)T * kTInfoWords + kTInfoPrefix];  // the tile's content prefix
-  const uint32_t ppre = tinfo[((size_t)f * ntile + G.tcum[p]) * kTInfoWords + kTInfoPrefix];
-  // the lane's block, and for the tile's last block the next tile's first
-  // (its header completes the last dword when the plane goes on)
   const bool live = tid < nloc;
-  const bool plane_end = g0 + nloc == G.cum[p + 1];
-  const uint32_t sz = live ? sizes[gb + tid] : 0u;
-  const uint32_t so = live ? srcoff[gb + tid] : 0u;
+  const bool plane_end = g0 + nloc == cum_p1;
+  // Round trip 1, every load unconditional (a guarded load is a branch with
+  // its own wait): the tile's and the plane's content prefixes, the lane's
+  // chunk size and source offset, and the source offset of the block after
+  // the tile (whose header completes the tile's last dword when the plane
+  // goes on; clamped to the tile's last block when it does not)
+  uint32_t x = tinfo[(size_t)T * kTInfoWords + kTInfoPrefix];  // the tile's content prefix
+  uint32_t ppre = tinfo[((size_t)f * ntile + tcum_p) * kTInfoWords + kTInfoPrefix];
+  const uint32_t gl = gb + min(tid, nloc - 1);
+  uint32_t sz0 = sizes[gl], so0 = srcoff[gl];
+  uint32_t so1 = srcoff[gb + (plane_end ? nloc - 1 : nloc)];
+  // (consumed here, so the compiler issues them together and waits once,
+  // instead of sinking each scalar load to its first use)
+  asm volatile("" : "+s"(x), "+s"(ppre), "+s"(so1), "+v"(sz0), "+v"(so0));
+  if (surplus) return;
+  const uint32_t sz = live ? sz0 : 0u;
+  const uint32_t so = live ? so0 : 0u;
   const uint32_t* src;
   uint32_t sh;  // source byte misalignment
   if (so == kSrcOverflow) {
@@ -316,30 +360,31 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
     src = stage + (size_t)win_first_tile(T) * (kTileCap / 4) + (so >> 2);  // (window-relative)
     sh = so & 3u;
   }
-  uint32_t nxh = 0;  // the next tile's first header (lane nloc - 1, plane going on)
-  if (tid == nloc - 1 && !plane_end) {
-    const uint32_t so1 = srcoff[gb + nloc];
-    const uint32_t* s1 = so1 == kSrcOverflow ? oslots + (size_t)(gb + nloc) * kSlotWords
+  const uint32_t* s1 = plane_end ? stage
+                       : so1 == kSrcOverflow ? oslots + (size_t)(gb + nloc) * kSlotWords
                                              : stage + (size_t)win_first_tile(T + 1) * (kTileCap / 4) + (so1 >> 2);
-    const uint32_t r1 = so1 == kSrcOverflow ? 0u : so1 & 3u;
-    nxh = r1 ? (s1[0] >> (8 * r1)) | (s1[1] << (32 - 8 * r1)) : s1[0];
-  }
-  // source words 8 (+1) per load round trip; the first round also gives the
-  // chunk's header
+  const uint32_t r1 = plane_end || so1 == kSrcOverflow ? 0u : so1 & 3u;
+  // Round trip 2: source words 8 (+1) per round trip (the first round also
+  // gives the chunk's header; predicated per word: most chunks are a few
+  // words, and unconditional loads measured slower), and the next tile's
+  // first header
   const uint32_t nsrc = (sh + sz + 3) >> 2;
   uint32_t v[9];
 #pragma unroll
   for (uint32_t k = 0; k < 9; k++) v[k] = (k < nsrc) ? src[k] : 0u;
+  const uint32_t n0 = s1[0], n1 = s1[1];
+  const uint32_t nxh = plane_end ? 0u : (r1 ? (n0 >> (8 * r1)) | (n1 << (32 - 8 * r1)) : n0);
   const uint32_t hdr = sh ? (v[0] >> (8 * sh)) | (v[1] << (32 - 8 * sh)) : v[0];
-  // ---- offsets in the tile (block order), the next lane's header
-  const uint32_t incl = wave_inclusive_scan(sz);
+  // ---- offsets in the tile (block order), the next lane's header (the
+  // whole workgroup is active here: DPP forms)
+  const uint32_t incl = wave_inclusive_scan_dpp(sz);
   if (lane == 63) s_wt[wave] = incl;
   if (lane == 0) s_hdr[wave] = hdr;
   __syncthreads();
   uint32_t o = incl - sz;
 #pragma unroll
   for (uint32_t w = 0; w < 4; w++) o += w < wave ? s_wt[w] : 0u;
-  uint32_t nh = (uint32_t)__shfl_down((int)hdr, 1, 64);
+  uint32_t nh = wave_next_lane(hdr);
   if (lane == 63) nh = wave < 3 ? s_hdr[wave + 1] : 0u;
   if (tid == nloc - 1) nh = nxh;
   const bool has_next = tid + 1 < nloc || !plane_end;  // a chunk follows in this plane
@@ -347,7 +392,7 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
   const uint64_t spos = 12ull + 8ull * (p + 1) + ppre + g0;
   if (live && spos + tid < cap) out[spos + tid] = (uint8_t)sz;
   if (!live || sz == 0) return;
-  const uint64_t P = 12ull + 8ull * (p + 1) + G.cum[p + 1] + x + o;  // the chunk's stream position
+  const uint64_t P = 12ull + 8ull * (p + 1) + cum_p1 + x + o;  // the chunk's stream position
   if (P + sz > cap) return;  // (capacity: k_tile_scan reports it)
   // ---- chunk bytes k .. k+3 (from source byte sh + k), the next header after byte sz
   auto word_at = [&](uint32_t k, const uint32_t* w, uint32_t j0) -> uint32_t {
@@ -355,7 +400,7 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
     return q ? (w[i] >> (8 * q)) | (w[i + 1] << (32 - 8 * q)) : w[i];
   };
   const uint32_t lead = (uint32_t)((4u - (uint32_t)(P & 3u)) & 3u);  // chunk bytes before the first own dword
-  const bool plane_first = g0 + tid == G.cum[p];
+  const bool plane_first = g0 + tid == cum_p;
   if (plane_first && lead) {  // the dword before is shared with the size array
     const uint32_t w = word_at(0, v, 0);
     for (uint32_t k = 0; k < lead; k++) out[P + k] = (uint8_t)(w >> (8 * k));
