@@ -991,10 +991,30 @@ __device__ __forceinline__ uint32_t fresh_lane_id() {
   asm volatile("v_mbcnt_hi_u32_b32 %0, -1, %1" : "=v"(id) : "v"(lo));
   return id;
 }
-__device__ __forceinline__ int wave_max_ln(int v, uint32_t ln) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) v = max(v, __builtin_amdgcn_ds_bpermute((int)((ln ^ (uint32_t)d) << 2), v));
-  return v;
+
+// The wave's maximum and an inclusive sum by DPP, for the run loop of
+// k_huff_encode only: its control is wave-uniform (the run comes from a
+// readfirstlane, the class branches are uniform), so every lane is active
+// where these run.  Under a partial EXEC, inactive lanes would pass nothing
+// on (the round-3 DPP episode): ds_bpermute forms stay
+// wherever EXEC can be partial.
+__device__ __forceinline__ int wave_max_full(int v) {  // (v >= 0)
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false));  // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false));  // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false));  // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false));  // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ uint32_t wave_incl_sum_full(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
 }
 
 struct WinScratch {
@@ -1155,7 +1175,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
 #pragma unroll
     for (int c = kClassDead - 1; c >= 0; c--)
       if (wcls == kClassDead && __ballot(live && mc == (uint32_t)c) != 0) wcls = (uint32_t)c;
-    const int wmsz = max(wave_max_ln(live ? mm : 0, ln), 1);
+    const int wmsz = max(wave_max_full(live ? mm : 0), 1);
     EncState S;
     bool ok = false;
     // (the coefficients are loaded inside each class's branch: loaded before
@@ -1182,12 +1202,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     // every dword stored once (DenseWriter)
     const bool dense = live && ok;
     const uint32_t sz = dense ? S.size : 0u;
-    uint32_t incl = sz;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ln - (uint32_t)d) << 2), (int)incl);
-      if (ln >= (uint32_t)d) incl += o;
-    }
+    const uint32_t incl = wave_incl_sum_full(sz);
     const uint32_t off = incl - sz;
     const uint64_t dm = __ballot(dense);
     const uint64_t above = ln == 63 ? 0ull : dm & ~((2ull << ln) - 1ull);
