@@ -992,10 +992,10 @@ __device__ __forceinline__ uint32_t fresh_lane_id() {
   return id;
 }
 
-// The wave's maximum and an inclusive sum by DPP, for the run loop of
-// k_huff_encode only: its control is wave-uniform (the run comes from a
-// readfirstlane, the class branches are uniform), so every lane is active
-// where these run.  Under a partial EXEC, inactive lanes would pass nothing
+// The wave's maximum and an inclusive sum by DPP, for k_huff_encode's count
+// scan (wave 0 whole) and run loop only: the loop's control is wave-uniform
+// (the run comes from a readfirstlane, the class branches are uniform), so
+// every lane is active where these run.  Under a partial EXEC, inactive lanes would pass nothing
 // on (the round-3 DPP episode): ds_bpermute forms stay
 // wherever EXEC can be partial.
 __device__ __forceinline__ int wave_max_full(int v) {  // (v >= 0)
@@ -1124,12 +1124,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
       v[j] = idx < kScanVals ? sc.cnt[idx] : 0u;
       sum += v[j];
     }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = (uint32_t)__shfl_up((int)incl, d, 64);
-      if (lane >= (uint32_t)d) incl += o;
-    }
+    const uint32_t incl = wave_incl_sum_full(sum);  // (all of wave 0 active)
     uint32_t ex = incl - sum;
 #pragma unroll
     for (uint32_t j = 0; j < kScanPer; j++) {
