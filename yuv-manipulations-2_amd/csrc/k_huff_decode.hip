@@ -128,39 +128,46 @@ struct Table {
 template <class Chunk>
 __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T) {
   if (s < 3) return 12;
-  // the chunk's first 20 bytes in registers, loaded together (the group walk
-  // below is a chain of dependent byte reads: from registers, not one LDS
-  // round trip per group; a table of at most 8 symbols ends within them)
-  uint32_t hb[5];
-#pragma unroll
-  for (uint32_t k = 0; k < 5; k++) hb[k] = c.bits32(32u * k);
-  auto byte_at = [&](uint32_t i) -> uint32_t {
-    if (i < 20u) {
-      const uint32_t k = i >> 2;
-      const uint32_t w = k == 0 ? hb[0] : (k == 1 ? hb[1] : (k == 2 ? hb[2] : (k == 3 ? hb[3] : hb[4])));
-      return (w >> (8u * (i & 3u))) & 0xFFu;
-    }
-    return c.byte(i);
-  };
-  const uint32_t nbits = byte_at(0) | (byte_at(1) << 8);
-  const uint32_t tb = byte_at(2);
+  // the chunk's first 20 bytes in registers, loaded together: the group walk
+  // below is a chain of dependent byte reads, from registers for every table
+  // that ends within them (at most 8 symbols always do), from LDS for the
+  // rest in a second walk; both walks branch-free (a dynamic byte index as a
+  // select chain compiled to nested EXEC branches, ~90 instructions a group)
+  // (five named values, not an array: selects between an array's elements
+  // are turned into a dynamically indexed scratch array)
+  const uint32_t h0 = c.bits32(0), h1 = c.bits32(32), h2 = c.bits32(64), h3 = c.bits32(96), h4 = c.bits32(128);
+  const uint32_t nbits = h0 & 0xFFFFu;
+  const uint32_t tb = (h0 >> 16) & 0xFFu;
   if (nbits > 512 || 3 + tb + (nbits + 7) / 8 > s) return 12;
+  auto reg_byte = [=](uint32_t i) -> uint32_t {  // i < 20
+    const uint32_t k = i >> 2;
+    const uint32_t w01 = (k & 1u) ? h1 : h0;
+    const uint32_t w23 = (k & 1u) ? h3 : h2;
+    const uint32_t w = k >= 4u ? h4 : ((k & 2u) ? w23 : w01);
+    return (w >> (8u * (i & 3u))) & 0xFFu;
+  };
   uint64_t cnt = 0, glo = 0, ghi = 0;
   uint32_t seen = 0, total = 0, i = 3;
-  bool regular = true;
-  while (i - 3 < tb) {
-    const uint32_t info = byte_at(i);
+  bool regular = true, bad = false;
+  auto group = [&](uint32_t info) {  // the group whose info byte is at i
     const uint32_t L = (info >> 5) + 1, n = (info & 31) + 1;
     const uint32_t nbytes = (n * 11 + 7) / 8;
     total += n;
-    if (i + 1 + nbytes > 3 + tb || total > 64) return 12;
+    bad = bad || i + 1 + nbytes > 3 + tb || total > 64;
     cnt += (uint64_t)n << (8 * (L - 1));
-    if (seen & (1u << L)) regular = false;
+    regular = regular && !(seen & (1u << L));
     seen |= 1u << L;
     const uint64_t gb = (uint64_t)(8 * (i + 1)) << (16 * ((L - 1) & 3));
-    if (L <= 4) glo |= gb; else ghi |= gb;
+    glo |= L <= 4 ? gb : 0ull;
+    ghi |= L <= 4 ? 0ull : gb;
     i += 1 + nbytes;
+  };
+  if (3 + tb <= 20) {
+    while (i - 3 < tb && !bad) group(reg_byte(i));
+  } else {
+    while (i - 3 < tb && !bad) group(c.byte(i));
   }
+  if (bad) return 12;
   uint32_t F = 0;
 #pragma unroll
   for (int L = 0; L < 8; L++) {  // length L + 1
