@@ -689,18 +689,18 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
     // compacted block: the two slots differ (rrank < nrest <= 16u + lane).
     const bool mine = D.live && !isdc && (rrank >> 4) == u;
     if (mine) {
-      uint4* img = reinterpret_cast<uint4*>(tile + (rrank & 15u) * xf::kTile);
+      uint4* img = reinterpret_cast<uint4*>(tile + (rrank & 15u) * xf::kTile + xf::img_word(rrank & 15u));
 #pragma unroll
       for (int c = 0; c < 8; c++) img[c] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
     }
     if (lane < 16u && 16u * u + lane >= nrest) {
-      uint4* img = reinterpret_cast<uint4*>(tile + lane * xf::kTile);
+      uint4* img = reinterpret_cast<uint4*>(tile + lane * xf::kTile + xf::img_word(lane));
 #pragma unroll
       for (int c = 0; c < 8; c++) img[c] = make_uint4(0u, 0u, 0u, 0u);
     }
     xf::wave_sync();
     uint2 w0, w1;
-    xf::idct_rows(tile + b * xf::kTile, q, sq, w0, w1);
+    xf::idct_rows(tile + b * xf::kTile, q, b, sq, w0, w1);
     if (16u * u + b < nrest) {
       const uint32_t gl = D.g0 + s_blk[16u * u + b];  // the block of compacted position 16u + b
       const uint32_t off = xf::block_row_offset(U, gl - U.cum, 2u * q);

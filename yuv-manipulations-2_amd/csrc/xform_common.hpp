@@ -382,8 +382,15 @@ __device__ __forceinline__ void pack_quads(const uint32_t (&c)[16], uint32_t q, 
 // 2w, 2w+1) is the first 32 dwords of its transpose tile tb; Qt: the plane's
 // Q table (natural order).  Out: pixel rows 2q (w0) and 2q+1 (w1), 8 bytes
 // each.  Shared by k_dequant_idct and the fused decoder (k_decode_idct).
-__device__ __forceinline__ void idct_rows(float* tb, uint32_t q, const float* Qt, uint2& w0, uint2& w1) {
-  const uint32_t* tw = reinterpret_cast<const uint32_t*>(tb);
+// The int16 image of block slot b sits at word img_word(b) of its tile
+// region (the float tile at word 0): slots b and b + 4 of a 32-lane group
+// then start on different banks (72 b mod 32 repeats every 4 slots), so the
+// image's 16-B writes and idct_rows' word reads are conflict-free.
+__device__ __forceinline__ constexpr uint32_t img_word(uint32_t b) { return 4u * ((b >> 2) & 1u); }
+
+__device__ __forceinline__ void idct_rows(float* tb, uint32_t q, uint32_t b, const float* Qt, uint2& w0,
+                                          uint2& w1) {
+  const uint32_t* tw = reinterpret_cast<const uint32_t*>(tb) + img_word(b);
   // (Z[k][2q], Z[k][2q+1]) = word k*4 + q
   uint32_t zc[8];
 #pragma unroll
