@@ -201,3 +201,16 @@ def test_repeated_compress_stable(codec, tiled8k):
     img = myyuv_file.YUVFile(width=8192, height=8192, data=tiled8k)
     assert sha(img.compressed(bytes([90] * 3), pays[0]).dumps()) == \
         "6f0fcfaeeae152f764ed46c8c8973345cfffbe54e2e3850a8bf7ca792e85fc05"
+
+
+def test_tiled_16384x8192_tile_scan_reload_path(codec, oracle, chef_big):
+    """A frame with more K2 tiles than k_tile_scan keeps in registers (10,240
+    tiles > 256 threads x 32): its second pass reloads the tile totals in
+    batches.  Stream and decode against the oracle's."""
+    import synth
+    f, raw = chef_big
+    w, h = 16384, 8192
+    t = synth.tiled_frame(raw, f.width, f.height, w, h).tobytes()
+    pay = codec.compress(t, w, h, (50, 50, 50))
+    assert pay == oracle.compress(t, w, h, (50, 50, 50))
+    assert sha(codec.decompress(pay, w, h, (50, 50, 50))) == sha(oracle.decompress(pay, w, h, (50, 50, 50)))
