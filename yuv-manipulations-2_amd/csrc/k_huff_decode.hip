@@ -41,13 +41,17 @@ namespace myyuv_gpu {
 
 namespace {
 
-// 6 KiB stage: 96 B of chunk per block on average (a 4K frame at q=50 uses
+// 5 KiB stage: 80 B of chunk per block on average (a 4K frame at q=50 uses
 // ~12 B); a wave whose chunks do not fit is staged in several rounds.
-constexpr uint32_t kStageQuads = 384;
+constexpr uint32_t kStageQuads = 320;
 // One zero quad after the stage (zeroed at kernel start, never staged into):
 // the symbol loop reads a lane's value from it when the lane takes none, so
 // the value needs no select.
 constexpr uint32_t kZeroBit = kStageQuads * 128u;
+// after the zero quad: the table parse's per-lane value positions, 8 u16 per
+// lane (decode_regular reads one per symbol: an LDS read instead of a select
+// between 64-bit register pairs and a 64-bit shift, five VALU per symbol)
+constexpr uint32_t kGposQuads = 8 * 64 * 2 / 16;
 
 #ifndef MYYUV_K5_GROUP
 #define MYYUV_K5_GROUP 2  // positions per "any lane left" test (1 / 2 / 4 / 8: 132.4 / 128.2 / 129.0 / 135.1 us per launch, tools/runs/r3n.sh)
@@ -119,14 +123,13 @@ struct Table {
   uint32_t tb = 0;      // table bytes
   uint64_t cnt = 0;     // code count of length L in byte L-1
   uint32_t lim[4] = {0, 0, 0, 0};   // 16-bit fields: left-justified limit, lengths 2k+1, 2k+2
-  uint32_t gpos[4] = {0, 0, 0, 0};  // 16-bit fields: 4096 + group bit - 11 * first
   bool regular = true;
 };
 
 // Header + table (Huffman::fromDump, Huffman.cpp:243-277).  Returns 0 or the
 // MYYUV_E_* code (12: bad chunk).
 template <class Chunk>
-__device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T) {
+__device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T, uint16_t* gcol) {
   if (s < 3) return 12;
   // the chunk's first 20 bytes in registers, loaded together: the group walk
   // below is a chain of dependent byte reads, from registers for every table
@@ -177,7 +180,7 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T)
     const uint32_t gb = (uint32_t)((L < 4 ? glo : ghi) >> (16 * (L & 3))) & 0xFFFF;
     const uint32_t gp = (4096 + gb - 11 * F) & 0xFFFF;
     T.lim[L >> 1] |= lim << (16 * (L & 1));
-    T.gpos[L >> 1] |= gp << (16 * (L & 1));
+    gcol[64 * L] = (uint16_t)gp;
     F = (F + cL) << 1;
   }
   T.nbits = nbits;
@@ -208,7 +211,7 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T)
 // read by one position, measured no faster on MI355X, and with the loads
 // three positions ahead the decoded values came out wrong nondeterministically
 // in long straight-line groups: both are deliberately not done.)
-__device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T, bool act,
+__device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T, const uint16_t* gcol, bool act,
                                                uint32_t (&nw)[32]) {
   bool bad = false;
   uint32_t bp = 0;
@@ -216,8 +219,6 @@ __device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T
   act = act && T.nbits > 0;
   const uint32_t P0 = 8 * c.b0 + T.sbit;  // stage bit of the first symbol bit
   const uint32_t vbase = 8 * c.b0 - 4096;  // stage bit of chunk bit 0, less the gpos bias
-  const uint64_t glo = ((uint64_t)T.gpos[1] << 32) | T.gpos[0];
-  const uint64_t ghi = ((uint64_t)T.gpos[3] << 32) | T.gpos[2];
 #pragma unroll
   for (int j0 = 0; j0 < 64; j0 += MYYUV_K5_GROUP) {
     if (__ballot(act) == 0) continue;
@@ -237,8 +238,9 @@ __device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T
     const bool ok = n < 8 && bpn <= T.nbits;
     bad = bad || (act && !ok);
     const bool take = act && ok;
-    // the value: 16-bit field n of gpos (a 64-bit shift uses its count mod 64)
-    const uint32_t G = (uint32_t)((n < 4 ? glo : ghi) >> (n << 4)) & 0xFFFFu;
+    // the value: length n + 1's entry of the lane's column of the LDS table
+    // (n = 8, no match: any entry, the value is not taken)
+    const uint32_t G = gcol[64 * (n & 7u)];
     const uint32_t vbit = (w8 >> ((7 - n) & 7)) * 11u + G + vbase;
     const uint32_t P = take ? vbit : kZeroBit, w = P >> 5;  // (stage bits; kZeroBit: the zero quad)
     const uint32_t raw = funnel(c.st[w + 1], c.st[w], P);
@@ -373,6 +375,10 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   local_off += gbase;
   tile_pre += (size_t)f * (ntiles + 1);
   const int lane = threadIdx.x;
+  // the lanes' per-length value positions (4096 + group bit - 11 * first
+  // code; u16, length-major: lane l's length L at [64 L + l]), after the
+  // stage and its zero quad
+  uint16_t* gcol = reinterpret_cast<uint16_t*>(stq + kStageQuads + 1) + lane;
   const uint32_t t = blockIdx.x;
   const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
   // the plane's fields by static index (a dynamic index into the kernel
@@ -492,11 +498,11 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
     const LdsChunk lc{reinterpret_cast<const uint32_t*>(stq), mine ? cpos + rel - aw : 0u};
     Table T;
     int pcode = 0;
-    if (mine) pcode = parse_table(lc, s, T);
+    if (mine) pcode = parse_table(lc, s, T, gcol);
     const bool go = mine && pcode == 0;
     int dcode = 0;
     DSTAMP(2);
-    const bool failed = decode_regular(lc, T, go && T.regular, nw);
+    const bool failed = decode_regular(lc, T, gcol, go && T.regular, nw);
     // tables the reference never writes, and failed messages (for the
     // reference's exact error code): the bit-serial path
     if (go && (!T.regular || failed)) {
@@ -540,7 +546,7 @@ __global__ __launch_bounds__(64, MYYUV_K5S_WAVES) void k_huff_decode(const uint8
                                                    uint4* __restrict__ coef,
                                                    uint8_t* __restrict__ rmask,
                                                    unsigned long long* __restrict__ err) {
-  __shared__ uint4 stq[kStageQuads + 1];
+  __shared__ uint4 stq[kStageQuads + 1 + kGposQuads];
   if (threadIdx.x == 0) stq[kStageQuads] = make_uint4(0u, 0u, 0u, 0u);  // (ordered by decode_group's barrier)
   DecodeGroup D;
   uint32_t nw[32];
@@ -589,7 +595,7 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
                                                    uint8_t* __restrict__ frame,
                                                    unsigned long long* __restrict__ err) {
   static_assert(sizeof(uint4) * kStageQuads >= sizeof(float) * xf::kXfTile16, "the tile over the stage");
-  __shared__ uint4 stq[kStageQuads + 1];
+  __shared__ uint4 stq[kStageQuads + 1 + kGposQuads];
   __shared__ float sq[64];
   __shared__ uint16_t s_blk[64];
   const uint32_t lane = threadIdx.x;
