@@ -48,10 +48,11 @@ constexpr uint32_t kStageQuads = 320;
 // the symbol loop reads a lane's value from it when the lane takes none, so
 // the value needs no select.
 constexpr uint32_t kZeroBit = kStageQuads * 128u;
-// after the zero quad: the table parse's per-lane value positions, 8 u16 per
-// lane (decode_regular reads one per symbol: an LDS read instead of a select
-// between 64-bit register pairs and a 64-bit shift, five VALU per symbol)
-constexpr uint32_t kGposQuads = 8 * 64 * 2 / 16;
+// after the zero quad: the table parse's per-lane value positions, 8 u32 per
+// lane, length-major (decode_regular reads one per symbol, conflict-free:
+// an LDS read instead of a select between 64-bit register pairs, a 64-bit
+// shift and an add)
+constexpr uint32_t kGposQuads = 8 * 64 * 4 / 16;
 
 #ifndef MYYUV_K5_GROUP
 #define MYYUV_K5_GROUP 2  // positions per "any lane left" test (1 / 2 / 4 / 8: 132.4 / 128.2 / 129.0 / 135.1 us per launch, tools/runs/r3n.sh)
@@ -129,7 +130,7 @@ struct Table {
 // Header + table (Huffman::fromDump, Huffman.cpp:243-277).  Returns 0 or the
 // MYYUV_E_* code (12: bad chunk).
 template <class Chunk>
-__device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T, uint16_t* gcol) {
+__device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T, uint32_t* gcol) {
   if (s < 3) return 12;
   // the chunk's first 20 bytes in registers, loaded together: the group walk
   // below is a chain of dependent byte reads, from registers for every table
@@ -178,9 +179,8 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T,
     if (F + cL > (2u << L)) regular = false;
     const uint32_t lim = ((F + cL) << (7 - L)) & 0xFFFF;
     const uint32_t gb = (uint32_t)((L < 4 ? glo : ghi) >> (16 * (L & 3))) & 0xFFFF;
-    const uint32_t gp = (4096 + gb - 11 * F) & 0xFFFF;
     T.lim[L >> 1] |= lim << (16 * (L & 1));
-    gcol[64 * L] = (uint16_t)gp;
+    gcol[64 * L] = 8 * c.b0 + gb - 11 * F;  // (mod 2^32: the first value's stage bit is 8 b0 + gb)
     F = (F + cL) << 1;
   }
   T.nbits = nbits;
@@ -211,14 +211,13 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T,
 // read by one position, measured no faster on MI355X, and with the loads
 // three positions ahead the decoded values came out wrong nondeterministically
 // in long straight-line groups: both are deliberately not done.)
-__device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T, const uint16_t* gcol, bool act,
+__device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T, const uint32_t* gcol, bool act,
                                                uint32_t (&nw)[32]) {
   bool bad = false;
   uint32_t bp = 0;
   uint64_t rwin = 0;  // MSB-first window: the next symbol's first bit at bit 63
   act = act && T.nbits > 0;
   const uint32_t P0 = 8 * c.b0 + T.sbit;  // stage bit of the first symbol bit
-  const uint32_t vbase = 8 * c.b0 - 4096;  // stage bit of chunk bit 0, less the gpos bias
 #pragma unroll
   for (int j0 = 0; j0 < 64; j0 += MYYUV_K5_GROUP) {
     if (__ballot(act) == 0) continue;
@@ -238,10 +237,11 @@ __device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T
     const bool ok = n < 8 && bpn <= T.nbits;
     bad = bad || (act && !ok);
     const bool take = act && ok;
-    // the value: length n + 1's entry of the lane's column of the LDS table
-    // (n = 8, no match: any entry, the value is not taken)
+    // the value: the code's n + 1 bits times 11 plus length n + 1's entry of
+    // the lane's column of the LDS table, the stage bit of its length's first
+    // value less 11 times its first code (n = 8, no match: not taken)
     const uint32_t G = gcol[64 * (n & 7u)];
-    const uint32_t vbit = (w8 >> ((7 - n) & 7)) * 11u + G + vbase;
+    const uint32_t vbit = ((uint32_t)(rwin >> 32) >> ((31u - n) & 31u)) * 11u + G;
     const uint32_t P = take ? vbit : kZeroBit, w = P >> 5;  // (stage bits; kZeroBit: the zero quad)
     const uint32_t raw = funnel(c.st[w + 1], c.st[w], P);
     const uint32_t v = (uint32_t)(((int32_t)(raw << 21)) >> 21);
@@ -375,10 +375,10 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   local_off += gbase;
   tile_pre += (size_t)f * (ntiles + 1);
   const int lane = threadIdx.x;
-  // the lanes' per-length value positions (4096 + group bit - 11 * first
-  // code; u16, length-major: lane l's length L at [64 L + l]), after the
-  // stage and its zero quad
-  uint16_t* gcol = reinterpret_cast<uint16_t*>(stq + kStageQuads + 1) + lane;
+  // the lanes' per-length value positions (stage bit of the length's first
+  // value - 11 * its first code; length-major: lane l's length L at
+  // [64 L + l]), after the stage and its zero quad
+  uint32_t* gcol = reinterpret_cast<uint32_t*>(stq + kStageQuads + 1) + lane;
   const uint32_t t = blockIdx.x;
   const int p = t >= tiles_p0 ? (t >= tiles_p0 + tiles_p1 ? 2 : 1) : 0;
   // the plane's fields by static index (a dynamic index into the kernel
