@@ -112,8 +112,11 @@ __device__ __forceinline__ uint32_t unit_stride() { return gridDim.x * 4u; }
 // B(v, k) = D[v][k] (forward: T * D^T) or D[k][v] (inverse: U * D).
 // kSkip: a step k whose P[2k], P[2k+1] are zero in every lane of the wave is
 // skipped (the sums start at +0 and a +-0 product leaves a sum unchanged, so
-// the result is bit-identical; see K6).
-template <bool kInverse, bool kSkip = false>
+// the result is bit-identical; see K6).  kFence: the accumulators' updates
+// kept in round-robin order (fence16); across the skip branches the fence
+// pins the accumulators to registers that the two paths do not share, which
+// costs a copy of them at every join (the fused decoder leaves it out).
+template <bool kInverse, bool kSkip = false, bool kFence = true>
 __device__ __forceinline__ void dot_rows(const float (&P)[16], float (&out)[16]) {
   if (kSkip) {
 #pragma unroll
@@ -131,7 +134,7 @@ __device__ __forceinline__ void dot_rows(const float (&P)[16], float (&out)[16])
     }
 #pragma unroll
     for (int j = 0; j < 16; j++) out[j] = (k == 0 && !kSkip) ? pr[j] : out[j] + pr[j];
-    fence16(out);
+    if (kFence) fence16(out);
   }
 }
 
@@ -429,7 +432,8 @@ __device__ __forceinline__ void idct_rows(float* tb, uint32_t q, uint32_t b, con
     }
 #pragma unroll
     for (int j = 0; j < 16; j++) Um[j] = Um[j] + pr[j];
-    fence16(Um);
+    // (no fence16 here: across the skip branches it costs a copy of the
+    // accumulators at every join, see dot_rows)
   }
 
   // ---- transpose (the float tile reuses the block's LDS)
@@ -439,7 +443,7 @@ __device__ __forceinline__ void idct_rows(float* tb, uint32_t q, uint32_t b, con
   // ---- stage 2: R[i][v] = sum_k U[i][k] * D[k][v] (squareMatrixMul<8>(U, DCT)),
   // then clamp(roundf(R) + 128) (DCT.cpp:358-362)
   float S[16];  // S[2v + h] = R[2q + h][v]
-  dot_rows<true, true>(P, S);
+  dot_rows<true, true, false>(P, S);
   uint32_t px[16];  // low byte = pixel
   bool tie = false;  // an exact .5 in the lane: fract(s') == 0.5 (exact for |s'| <= 128)
 #pragma unroll
