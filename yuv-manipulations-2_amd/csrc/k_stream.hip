@@ -156,6 +156,11 @@ struct alignas(4) Dw4 {  // a 16-byte store at a dword-aligned address (global_s
   uint32_t x, y, z, w;
 };
 
+// k_stream_out: source words a lane loads in its first round trip (chunks of
+// up to 4 kVw - 3 bytes are copied from registers with static indices)
+constexpr uint32_t kVw = 16;
+typedef __attribute__((address_space(1))) uint32_t gu32;  // global loads, not flat
+
 __device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uint32_t* tile_pre,
                                             uint32_t g) {
   return local_off[g] + tile_pre[g / kScanTile];
@@ -364,14 +369,15 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
                        : so1 == kSrcOverflow ? oslots + (size_t)(gb + nloc) * kSlotWords
                                              : stage + (size_t)win_first_tile(T + 1) * (kTileCap / 4) + (so1 >> 2);
   const uint32_t r1 = plane_end || so1 == kSrcOverflow ? 0u : so1 & 3u;
-  // Round trip 2: source words 8 (+1) per round trip (the first round also
-  // gives the chunk's header; predicated per word: most chunks are a few
-  // words, and unconditional loads measured slower), and the next tile's
-  // first header
+  // Round trip 2: the chunk's first kVw source words (every chunk of the
+  // bench frame: its longest is 55 bytes; predicated per word: most chunks
+  // are a few words, and unconditional loads measured slower), which also
+  // give its header, and the next tile's first header
   const uint32_t nsrc = (sh + sz + 3) >> 2;
-  uint32_t v[9];
+  const gu32* gsrc = (const gu32*)src;
+  uint32_t v[kVw];
 #pragma unroll
-  for (uint32_t k = 0; k < 9; k++) v[k] = (k < nsrc) ? src[k] : 0u;
+  for (uint32_t k = 0; k < kVw; k++) v[k] = (k < nsrc) ? gsrc[k] : 0u;
   const uint32_t n0 = s1[0], n1 = s1[1];
   const uint32_t nxh = plane_end ? 0u : (r1 ? (n0 >> (8 * r1)) | (n1 << (32 - 8 * r1)) : n0);
   const uint32_t hdr = sh ? (v[0] >> (8 * sh)) | (v[1] << (32 - 8 * sh)) : v[0];
@@ -394,18 +400,59 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
   if (!live || sz == 0) return;
   const uint64_t P = 12ull + 8ull * (p + 1) + cum_p1 + x + o;  // the chunk's stream position
   if (P + sz > cap) return;  // (capacity: k_tile_scan reports it)
-  // ---- chunk bytes k .. k+3 (from source byte sh + k), the next header after byte sz
+  const uint32_t lead = (uint32_t)((4u - (uint32_t)(P & 3u)) & 3u);  // chunk bytes before the first own dword
+  const bool plane_first = g0 + tid == cum_p;
+  if (plane_first && lead) {  // the dword before is shared with the size array
+    for (uint32_t k = 0; k < lead; k++) out[P + k] = (uint8_t)(hdr >> (8 * k));  // (hdr: chunk bytes 0..3)
+  }
+  if (sh + sz <= 4u * kVw) {
+    // ---- the chunk in registers: a[m] = chunk bytes lead + 4m .. +3, i.e.
+    // source bytes d + 4m (d = sh + lead <= 6: word i0 + m, shifted by qb) —
+    // static indices only (a per-lane index into v[] is a select chain)
+    const uint32_t d = sh + lead, qb = d & 3u;
+    const bool i1 = d >= 4u;
+    uint32_t u[kVw + 1], a[kVw];
+#pragma unroll
+    for (uint32_t m = 0; m < kVw; m++) u[m] = i1 ? (m + 1 < kVw ? v[m + 1] : 0u) : v[m];
+    u[kVw] = 0u;
+#pragma unroll
+    for (uint32_t m = 0; m < kVw; m++) a[m] = __builtin_amdgcn_alignbyte(u[m + 1], u[m], qb);
+    const uint32_t nb = sz > lead ? sz - lead : 0u;  // chunk bytes from the first own dword
+    const uint32_t nq = nb >> 4, nt = (nb >> 2) & 3u, rem = nb & 3u;
+    uint8_t* o = out + P + lead;  // (4-byte aligned)
+#pragma unroll
+    for (uint32_t it = 0; it < kVw / 4; it++)
+      if (it < nq) *reinterpret_cast<Dw4*>(o + 16 * it) = Dw4{a[4 * it], a[4 * it + 1], a[4 * it + 2], a[4 * it + 3]};
+    // the words after the last whole quad (4nq .. 4nq + nt - 1), then the
+    // partial word 4nq + nt completed with the next chunk's first bytes
+    uint32_t g[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) g[j] = nq & 2u ? (nq & 1u ? a[12 + j] : a[8 + j]) : (nq & 1u ? a[4 + j] : a[j]);
+    uint8_t* ot = o + 16 * nq;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; j++)
+      if (j < nt) *reinterpret_cast<uint32_t*>(ot + 4 * j) = g[j];
+    if (rem) {
+      const uint32_t w = nt & 2u ? (nt & 1u ? g[3] : g[2]) : (nt & 1u ? g[1] : g[0]);
+      const uint64_t pk = P + sz - rem;  // = ot + 4 nt
+      if (has_next && pk + 4 <= cap) {
+        *reinterpret_cast<uint32_t*>(out + pk) = (w & ((1u << (8 * rem)) - 1u)) | (nh << (8 * rem));
+      } else {  // the plane's last chunk (the next plane's header follows), or the end of `cap`
+        for (uint32_t i = 0; i < rem; i++) out[pk + i] = (uint8_t)(w >> (8 * i));
+      }
+    }
+    return;
+  }
+  // ---- longer chunks (overflow slots, up to 160 bytes): chunk bytes k ..
+  // k+3 from source byte sh + k, 9 source words at a time
   auto word_at = [&](uint32_t k, const uint32_t* w, uint32_t j0) -> uint32_t {
     const uint32_t r = sh + k, i = (r >> 2) - j0, q = r & 3u;
     return q ? (w[i] >> (8 * q)) | (w[i + 1] << (32 - 8 * q)) : w[i];
   };
-  const uint32_t lead = (uint32_t)((4u - (uint32_t)(P & 3u)) & 3u);  // chunk bytes before the first own dword
-  const bool plane_first = g0 + tid == cum_p;
-  if (plane_first && lead) {  // the dword before is shared with the size array
-    const uint32_t w = word_at(0, v, 0);
-    for (uint32_t k = 0; k < lead; k++) out[P + k] = (uint8_t)(w >> (8 * k));
-  }
-  uint32_t j0 = 0;  // first source word held in v
+  uint32_t r[9];  // source words j0 .. j0 + 8
+#pragma unroll
+  for (uint32_t i = 0; i < 9; i++) r[i] = v[i];
+  uint32_t j0 = 0;
   uint32_t k = lead;
   // 16 chunk bytes per store while 16 remain (the wave's loop runs to its
   // longest chunk: a quarter of the iterations of dword stores)
@@ -414,9 +461,9 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
     if (need + 4 >= j0 + 9) {  // refill
       j0 = need;
 #pragma unroll
-      for (uint32_t i = 0; i < 9; i++) v[i] = (j0 + i < nsrc) ? src[j0 + i] : 0u;
+      for (uint32_t i = 0; i < 9; i++) r[i] = (j0 + i < nsrc) ? gsrc[j0 + i] : 0u;
     }
-    const Dw4 o{word_at(k, v, j0), word_at(k + 4, v, j0), word_at(k + 8, v, j0), word_at(k + 12, v, j0)};
+    const Dw4 o{word_at(k, r, j0), word_at(k + 4, r, j0), word_at(k + 8, r, j0), word_at(k + 12, r, j0)};
     *reinterpret_cast<Dw4*>(out + P + k) = o;  // (4-byte aligned: P + lead is)
   }
   for (; k < sz; k += 4) {
@@ -424,9 +471,9 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
     if (need + 1 >= j0 + 9) {  // refill (chunks over ~28 bytes)
       j0 = need;
 #pragma unroll
-      for (uint32_t i = 0; i < 9; i++) v[i] = (j0 + i < nsrc) ? src[j0 + i] : 0u;
+      for (uint32_t i = 0; i < 9; i++) r[i] = (j0 + i < nsrc) ? gsrc[j0 + i] : 0u;
     }
-    uint32_t w = word_at(k, v, j0);
+    uint32_t w = word_at(k, r, j0);
     const uint32_t rem = sz - k;
     if (rem >= 4) {
       *reinterpret_cast<uint32_t*>(out + P + k) = w;
