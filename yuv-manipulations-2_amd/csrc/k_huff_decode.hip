@@ -578,11 +578,11 @@ __global__ __launch_bounds__(64, MYYUV_K5S_WAVES) void k_huff_decode(const uint8
 }
 
 // Fused decoder (K5 + K6; MYYUV_DECODER=fused): the wave decodes its 64-block
-// group as K5 does, then runs K6's transform on it as four 16-block units
-// straight from its registers: the unit's 16 decoding lanes write their
-// blocks' int16 images into the wave's transpose tile (laid over the chunk
-// stage, dead by then), and the wave's lanes take K6's (block, quarter)
-// roles (idct_rows, xform_common.hpp).  The coefficients never reach HBM.
+// group as K5 does, then runs K6's transform on it in 8-block units straight
+// from its registers: the unit's 8 decoding lanes write their blocks' int16
+// images into the wave's transpose tile (laid over the chunk stage, dead by
+// then), and the wave's lanes take (block, row) roles (idct_row8,
+// xform_common.hpp).  The coefficients never reach HBM.
 __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_t* __restrict__ in,
                                                    const uint32_t* __restrict__ in_size,
                                                    uint32_t cap,
@@ -644,8 +644,8 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
   // basis is one value c, so R = fl(fl(c * z) * c) for all 64 pixels — the
   // same two roundings as the full transform, which the lane evaluates for its
   // own block and stores as 8 rows.  The other blocks are compacted into
-  // 16-block units for K6's transform (one to four units instead of always
-  // four; their rows are written wherever the blocks lie).
+  // 8-block units for the transform (up to eight; their rows are written
+  // wherever the blocks lie).
   const int p = D.p;
   xf::Unit U;
   U.p = p;
@@ -686,34 +686,51 @@ __global__ __launch_bounds__(64, MYYUV_K5_WAVES) void k_decode_idct(const uint8_
   const uint32_t rrank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rest >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rest, 0u));
   if (D.live && !isdc) s_blk[rrank] = (uint16_t)lane;  // compacted position -> the block's lane in the group
   float* tile = reinterpret_cast<float*>(stq);
-  const uint32_t q = lane & 3u, b = lane >> 2;
+  // 16-block units while more than 8 blocks are left (lane (b, q): rows 2q,
+  // 2q+1 of block b, idct_rows), the last 1-8 blocks as one 8-block unit
+  // (lane (b, r): row r, idct_row8, half the products per step).  Slots past
+  // the last block are zero, so they do not keep steps alive; slot `lane` is
+  // zeroed by lane `lane` whether or not that lane also writes a compacted
+  // block: the two slots differ (rrank < nrest <= base + lane).
 #pragma unroll 1
-  for (uint32_t u = 0; 16u * u < nrest; u++) {
-    // the unit's blocks: compacted positions 16u .. 16u+15 (slots past the
-    // last block are zero, so they do not keep steps alive).  Slot `lane`
-    // (< 16) is zeroed by lane `lane` whether or not that lane also writes a
-    // compacted block: the two slots differ (rrank < nrest <= 16u + lane).
-    const bool mine = D.live && !isdc && (rrank >> 4) == u;
-    if (mine) {
-      uint4* img = reinterpret_cast<uint4*>(tile + (rrank & 15u) * xf::kTile + xf::img_word(rrank & 15u));
+  for (uint32_t base = 0; base < nrest;) {
+    const bool wide = nrest - base > 8u;
+    const uint32_t span = wide ? 16u : 8u, stride = wide ? (uint32_t)xf::kTile : (uint32_t)xf::kTile8;
+    const uint32_t s = rrank - base;
+    if (D.live && !isdc && rrank >= base && s < span) {
+      uint4* img = reinterpret_cast<uint4*>(tile + s * stride + (wide ? xf::img_word(s) : 0u));
 #pragma unroll
       for (int c = 0; c < 8; c++) img[c] = make_uint4(nw[4 * c], nw[4 * c + 1], nw[4 * c + 2], nw[4 * c + 3]);
     }
-    if (lane < 16u && 16u * u + lane >= nrest) {
-      uint4* img = reinterpret_cast<uint4*>(tile + lane * xf::kTile + xf::img_word(lane));
+    if (lane < span && base + lane >= nrest) {
+      uint4* img = reinterpret_cast<uint4*>(tile + lane * stride + (wide ? xf::img_word(lane) : 0u));
 #pragma unroll
       for (int c = 0; c < 8; c++) img[c] = make_uint4(0u, 0u, 0u, 0u);
     }
     xf::wave_sync();
-    uint2 w0, w1;
-    xf::idct_rows(tile + b * xf::kTile, q, b, sq, w0, w1);
-    if (16u * u + b < nrest) {
-      const uint32_t gl = D.g0 + s_blk[16u * u + b];  // the block of compacted position 16u + b
-      const uint32_t off = xf::block_row_offset(U, gl - U.cum, 2u * q);
-      *reinterpret_cast<uint2*>(fr + off) = w0;
-      *reinterpret_cast<uint2*>(fr + off + U.pw) = w1;
+    if (wide) {
+      const uint32_t q = lane & 3u, b = lane >> 2;
+      uint2 w0, w1;
+      xf::idct_rows(tile + b * xf::kTile, q, b, sq, w0, w1);
+      if (base + b < nrest) {
+        const uint32_t gl = D.g0 + s_blk[base + b];  // the block of compacted position base + b
+        const uint32_t off = xf::block_row_offset(U, gl - U.cum, 2u * q);
+        *reinterpret_cast<uint2*>(fr + off) = w0;
+        *reinterpret_cast<uint2*>(fr + off + U.pw) = w1;
+      }
+    } else {
+      const uint32_t r = lane & 7u, b = lane >> 3;
+      float qc[8];  // the lane's column of the plane's Q table, Q[k][r]
+#pragma unroll
+      for (int k = 0; k < 8; k++) qc[k] = sq[8 * k + r];
+      const uint2 w = xf::idct_row8(tile + b * xf::kTile8, r, qc);
+      if (base + b < nrest) {
+        const uint32_t gl = D.g0 + s_blk[base + b];
+        *reinterpret_cast<uint2*>(fr + xf::block_row_offset(U, gl - U.cum, r)) = w;
+      }
     }
     xf::wave_sync();  // the next unit rewrites the tile
+    base += span;
   }
   DSTAMP(5);
 #ifdef MYYUV_STAMPS

@@ -479,5 +479,78 @@ __device__ __forceinline__ void idct_rows(float* tb, uint32_t q, uint32_t b, con
                                                     0x05040100u));
 }
 
+// The same transform on 8-block units, eight lanes per block (the fused
+// decoder's last 1-8 blocks of a group): lane (b, r) computes column r of U
+// in stage 1 and row r of R in stage 2, one pixel row per lane.  A step costs
+// 8 products and sums per lane instead of 16, so the last unit of a group
+// costs about two thirds of a 16-block one when it has 8 blocks or fewer
+// (half the VALU, the same LDS round trips).  All-8-block units measured
+// slower: 4.2 units per 64-block group instead of 2.3 (16.3 + 15.8 steps
+// instead of 10.0 + 9.6, tools/diag/idct_units.py), and each unit's fixed
+// round trips outweigh the halved steps (transform phase +22 %,
+// profiles/r5ai_*).  Slot b's region: kTile8 floats, its int16 image
+// (natural order) at word 0, the float tile over it after the image is read;
+// row stride 8, slot stride 72 (= 8 mod 32: the column writes of four slots
+// fall on distinct banks).  qc[k] = Q[k][r].
+constexpr int kTile8 = 72;
+constexpr int kAlways8 = 2;  // steps run without the skip test (row / column 0, 1: 100 / 97 % of the units)
+__device__ __forceinline__ uint2 idct_row8(float* tb, uint32_t r, const float (&qc)[8]) {
+  const int16_t* im = reinterpret_cast<const int16_t*>(tb);
+  int zk[8];  // Z[k][r]
+#pragma unroll
+  for (int k = 0; k < 8; k++) zk[k] = im[8 * k + r];
+  wave_sync();
+  // ---- dequantise (DCT.cpp:331) and stage 1, U[i][r] = sum_k D[k][i] * Z[k][r]
+  // (squareMatrixMulT2<8>(DCT, Z), DCT.cpp:256-266), k ascending; a row k
+  // that is zero in every block of the unit adds only +-0 products to sums
+  // that start at +0, so the wave skips it (bit-exact, see idct_rows)
+  float Um[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) Um[i] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (k >= kAlways8 && !__any(zk[k] != 0)) continue;
+    const float z = (float)zk[k] * qc[k];
+#pragma unroll
+    for (int i = 0; i < 8; i++) Um[i] = Um[i] + c_dct[k * 8 + i] * z;
+  }
+  // ---- transpose through the slot's tile: column r out, row r back
+#pragma unroll
+  for (int i = 0; i < 8; i++) tb[8 * i + r] = Um[i];
+  wave_sync();
+  const float4 p0 = *reinterpret_cast<const float4*>(tb + 8 * r);
+  const float4 p1 = *reinterpret_cast<const float4*>(tb + 8 * r + 4);
+  const float P[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};  // U[r][k]
+  // ---- stage 2: R[r][v] = sum_k U[r][k] * D[k][v] (squareMatrixMul<8>(U, DCT)),
+  // skipping the columns that are zero in every block, then
+  // clamp(roundf(R) + 128) (DCT.cpp:358-362)
+  float S[8];
+#pragma unroll
+  for (int v = 0; v < 8; v++) S[v] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (k >= kAlways8 && !__any(P[k] != 0.0f)) continue;
+#pragma unroll
+    for (int v = 0; v < 8; v++) S[v] = S[v] + P[k] * c_dct[k * 8 + v];
+  }
+  uint32_t px[8];
+  bool tie = false;
+#pragma unroll
+  for (int v = 0; v < 8; v++) {
+    S[v] = __builtin_amdgcn_fmed3f(S[v], -128.0f, 127.0f);
+    tie = tie || __builtin_amdgcn_fractf(S[v]) == 0.5f;
+    px[v] = bits(S[v] + kMagicPx);
+  }
+  if (tie) {
+#pragma unroll
+    for (int v = 0; v < 8; v++)
+      px[v] = (uint32_t)((int)__builtin_truncf(S[v] + __builtin_copysignf(kHalfDown, S[v])) + 128);
+  }
+  return make_uint2(__builtin_amdgcn_perm(__builtin_amdgcn_perm(px[3], px[2], 0x0c0c0400u),
+                                          __builtin_amdgcn_perm(px[1], px[0], 0x0c0c0400u), 0x05040100u),
+                    __builtin_amdgcn_perm(__builtin_amdgcn_perm(px[7], px[6], 0x0c0c0400u),
+                                          __builtin_amdgcn_perm(px[5], px[4], 0x0c0c0400u), 0x05040100u));
+}
+
 }  // namespace xf
 }  // namespace myyuv_gpu
