@@ -131,7 +131,9 @@ struct Table {
 // MYYUV_E_* code (12: bad chunk).
 template <class Chunk>
 __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T, uint32_t* gcol) {
-  if (s < 3) return 12;
+  // (no early returns: a bad header only sets `bad`, and the walk and the
+  // per-length pass run on whatever was read (inside the stage); each return
+  // path would otherwise re-initialise the outputs at its branch level)
   // the chunk's first 20 bytes in registers, loaded together: the group walk
   // below is a chain of dependent byte reads, from registers for every table
   // that ends within them (at most 8 symbols always do), from LDS for the
@@ -142,7 +144,7 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T,
   const uint32_t h0 = c.bits32(0), h1 = c.bits32(32), h2 = c.bits32(64), h3 = c.bits32(96), h4 = c.bits32(128);
   const uint32_t nbits = h0 & 0xFFFFu;
   const uint32_t tb = (h0 >> 16) & 0xFFu;
-  if (nbits > 512 || 3 + tb + (nbits + 7) / 8 > s) return 12;
+  const bool bad_hdr = s < 3 || nbits > 512 || 3 + tb + (nbits + 7) / 8 > s;
   auto reg_byte = [=](uint32_t i) -> uint32_t {  // i < 20
     const uint32_t k = i >> 2;
     const uint32_t w01 = (k & 1u) ? h1 : h0;
@@ -152,7 +154,7 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T,
   };
   uint64_t cnt = 0, glo = 0, ghi = 0;
   uint32_t seen = 0, total = 0, i = 3;
-  bool regular = true, bad = false;
+  bool regular = true, bad = bad_hdr;
   auto group = [&](uint32_t info) {  // the group whose info byte is at i
     const uint32_t L = (info >> 5) + 1, n = (info & 31) + 1;
     const uint32_t nbytes = (n * 11 + 7) / 8;
@@ -171,7 +173,6 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T,
   } else {
     while (i - 3 < tb && !bad) group(c.byte(i));
   }
-  if (bad) return 12;
   uint32_t F = 0;
 #pragma unroll
   for (int L = 0; L < 8; L++) {  // length L + 1
@@ -188,7 +189,7 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T,
   T.tb = tb;
   T.cnt = cnt;
   T.regular = regular;
-  return 0;
+  return bad ? 12 : 0;
 }
 
 // Symbols of REGULAR tables (Huffman.cpp:106-154) into nw (natural-order
@@ -497,8 +498,10 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
     const bool mine = ((pending >> lane) & 1) && cpos + rel + s <= wend;
     const LdsChunk lc{reinterpret_cast<const uint32_t*>(stq), mine ? cpos + rel - aw : 0u};
     Table T;
-    int pcode = 0;
-    if (mine) pcode = parse_table(lc, s, T, gcol);
+    // (every lane parses, the others as a bad header of size 0 at the stage's
+    // start: no branch level around the parse, whose outputs the compiler
+    // would re-initialise on the skipped path)
+    const int pcode = parse_table(lc, mine ? s : 0u, T, gcol);
     const bool go = mine && pcode == 0;
     int dcode = 0;
     DSTAMP(2);
