@@ -191,6 +191,7 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
   constexpr uint32_t kTsKeep = 32;
   __shared__ uint32_t s_w[4];
   __shared__ uint32_t s_carry;
+  __shared__ uint32_t s_pp[3];  // the content prefixes at the planes' first tiles
   const uint32_t f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t ntile = G.tcum[3];
   const uint32_t per = (ntile + 255) / 256;
@@ -232,8 +233,9 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
       for (uint32_t j = 0; j < kTsBatch; j++) v += x[j];
     }
   }
-  const uint32_t incl = wave_inclusive_scan(v);
+  const uint32_t incl = wave_inclusive_scan_dpp(v);  // (every thread active)
   if (lane == 63) s_w[wave] = incl;
+  if (tid == 0) s_pp[0] = 0u;
   __syncthreads();
   uint32_t pre = 0, tot = 0;
 #pragma unroll
@@ -248,6 +250,8 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
       const uint32_t t = tid * per + j;
       if (j < per && t < ntile) {
         info[(size_t)t * kTInfoWords + kTInfoPrefix] = pre;
+        if (t == G.tcum[1]) s_pp[1] = pre;
+        if (t == G.tcum[2]) s_pp[2] = pre;
         pre += keep[j];
       }
     }
@@ -260,6 +264,8 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
         const uint32_t t = tid * per + k0 + j;
         if (k0 + j < per && t < ntile) {
           info[(size_t)t * kTInfoWords + kTInfoPrefix] = pre;
+          if (t == G.tcum[1]) s_pp[1] = pre;
+          if (t == G.tcum[2]) s_pp[2] = pre;
           pre += x[j];
         }
       }
@@ -267,13 +273,13 @@ __global__ __launch_bounds__(256) void k_tile_scan(uint32_t* __restrict__ tinfo,
   }
   if (tid == 0) s_carry = tot;
   __syncthreads();
-  // plane headers: the prefixes at the planes' first tiles (written above by
-  // this workgroup; __syncthreads orders them)
+  // plane headers: the prefixes at the planes' first tiles (kept in LDS by
+  // their threads above; __syncthreads orders them; no read back of tinfo)
   if (tid < 3) {
     const int p = (int)tid;
     const uint32_t total = s_carry;
-    const uint32_t ppre = info[(size_t)G.tcum[p] * kTInfoWords + kTInfoPrefix];
-    const uint32_t pend = p < 2 ? info[(size_t)G.tcum[p + 1] * kTInfoWords + kTInfoPrefix] : total;
+    const uint32_t ppre = s_pp[p];
+    const uint32_t pend = p < 2 ? s_pp[p + 1] : total;
     const uint32_t nb = G.cum[p + 1] - G.cum[p], content = pend - ppre;
     uint8_t* o = out + (size_t)f * cap;
     const uint64_t hpos = 12ull + 8ull * p + G.cum[p] + ppre;
