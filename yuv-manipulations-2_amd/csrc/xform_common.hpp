@@ -493,7 +493,10 @@ __device__ __forceinline__ void idct_rows(float* tb, uint32_t q, uint32_t b, con
 // row stride 8, slot stride 72 (= 8 mod 32: the column writes of four slots
 // fall on distinct banks).  qc[k] = Q[k][r].
 constexpr int kTile8 = 72;
-constexpr int kAlways8 = 2;  // steps run without the skip test (row / column 0, 1: 100 / 97 % of the units)
+#ifndef MYYUV_ALWAYS8
+#define MYYUV_ALWAYS8 2
+#endif
+constexpr int kAlways8 = MYYUV_ALWAYS8;  // steps run without the skip test (row / column 0, 1: 100 / 97 % of the units)
 __device__ __forceinline__ uint2 idct_row8(float* tb, uint32_t r, const float (&qc)[8]) {
   const int16_t* im = reinterpret_cast<const int16_t*>(tb);
   int zk[8];  // Z[k][r]
