@@ -1,0 +1,13 @@
+# round 5: K2's window prologue: the frame geometry by static index (no chain
+# of dependent kernel-argument loads), unconditional block-word loads, the
+# classification as a waterfall over the keys present: GPU tests, K2's
+# window phases (stamp build), per-kernel times and the bench A/B against the
+# previous commit (build_var/base)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r5at_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r5at_tests.log; exit 1; }
+tail -1 gpurun_out/r5at_tests.log
+MYYUV_HIP_LIB=$GRAFT_REPO_ROOT/build_var/stamps/libmyyuv_hip.so timeout -k 10 200 python3 tools/k2_phase.py 24 > gpurun_out/r5at_k2_phase.txt 2>&1; cat gpurun_out/r5at_k2_phase.txt
+K1AB_B=24 timeout -k 10 300 python3 tools/k1_ab.py default build_var/base > gpurun_out/r5at_kab.txt 2>&1; cat gpurun_out/r5at_kab.txt
+timeout -k 10 500 bash tools/ab_bench.sh default build_var/base > /dev/null && cp gpurun_out/ab_bench.txt gpurun_out/r5at_ab.txt && cat gpurun_out/r5at_ab.txt

@@ -87,6 +87,19 @@ __device__ uint32_t g_k2_fstamps[8192 * 8];
     }                                                                                \
     _tprev = _t;                                                                     \
   } while (0)
+// K2's window phases per wave: [5] tiles, block words and classification,
+// [0] the rest of the prologue (count scan, sort, three barriers),
+// [1] runs' fetch + load + build, [2] runs' emission and lists, [3] runs,
+// [4] the last fetch + epilogue, [7] = 1 (g_k2_win[wave][8])
+__device__ uint32_t g_k2_win[65536 * 8];
+#define KWSTAMP(k)                                                                   \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();                            \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    _kw[(k)] += (uint32_t)(_t - _kwprev);                                            \
+    _kwprev = _t;                                                                    \
+  } while (0)
 // wave encoder: per-block phase cycles into g_k2_wstamps[block slot][8]
 // (plain stores: contended atomics would distort the timing)
 __device__ uint32_t g_k2_wstamps[65536 * 8];
@@ -1062,6 +1075,10 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
                                                          uint32_t* __restrict__ work_count) {
   __shared__ WinScratch sc;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+#ifdef MYYUV_STAMPS
+  uint32_t _kw[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+  unsigned long long _kwprev = __builtin_amdgcn_s_memtime();
+#endif
   const uint32_t NT = G.nframes * G.tcum[3];
   const uint32_t T0 = blockIdx.x * kWinTiles;
   // ---- the window's tiles (wave-uniform)
@@ -1114,6 +1131,9 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     }
     ent[k] = cls | (m << 3) | (rm << 10) | (rk << 18) | (key << 24);
   }
+#ifdef MYYUV_STAMPS
+  KWSTAMP(5);
+#endif
   __syncthreads();
   // ---- 2. exclusive scan of the counts in (key, round, wave) order (wave 0)
   if (wave == 0) {
@@ -1147,6 +1167,9 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   const uint32_t nlive = sc.cnt[kDeadKey * kWinRuns];
   __syncthreads();
   const uint32_t nruns = (nlive + kWave - 1) / kWave;
+#ifdef MYYUV_STAMPS
+  KWSTAMP(0);
+#endif
   // ---- 3. the runs, heaviest first
   while (true) {
     uint32_t r = 0;
@@ -1193,6 +1216,9 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
       R.load(coef, zq, live ? mg : 0u, live ? mrm : 0u);
       if (live) ok = build_r<8>(R, mm, wmsz, S);
     }
+#ifdef MYYUV_STAMPS
+    KWSTAMP(1);
+#endif
     // the run's chunks back to back (offsets by a wave scan of the sizes),
     // every dword stored once (DenseWriter)
     const bool dense = live && ok;
@@ -1221,6 +1247,10 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
       base = __builtin_amdgcn_readfirstlane(base);
       if ((ovf >> ln) & 1) work[base + lanes_below(ovf)] = mg;
     }
+#ifdef MYYUV_STAMPS
+    KWSTAMP(2);
+    _kw[3] += 1;
+#endif
   }
   // ---- 4. the last wave out publishes the tiles' dense bytes
   uint32_t d = 0;
@@ -1236,6 +1266,13 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
       info[4] = 0u;
     }
   }
+#ifdef MYYUV_STAMPS
+  KWSTAMP(4);
+  {
+    const uint32_t wid = blockIdx.x * (kK2Group / kWave) + wave;
+    if (lane < 8 && wid < 65536) g_k2_win[wid * 8 + lane] = lane < 6 ? _kw[lane < 6 ? lane : 0] : (lane == 7 ? 1u : 0u);
+  }
+#endif
 }
 
 // Fused single-pass encoder: K1 + K2 for one tile, the

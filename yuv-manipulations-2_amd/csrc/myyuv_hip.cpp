@@ -65,6 +65,7 @@ extern __device__ unsigned long long g_k2_stamps[40];
 extern __device__ uint32_t g_k2_wstamps[65536 * 8];
 extern __device__ uint32_t g_k2_fstamps[8192 * 8];
 extern __device__ uint32_t g_dec_wstamps[65536 * 8];
+extern __device__ uint32_t g_k2_win[65536 * 8];
 #endif
 }  // namespace myyuv_gpu
 
@@ -1019,6 +1020,22 @@ int myyuv_debug_k2_fstamps(uint32_t* out, uint32_t n) {
 #ifdef MYYUV_STAMPS
   if (n > 8192) n = 8192;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_fstamps), (size_t)n * 32) == hipSuccess ? 0 : MYYUV_E_HIP;
+#else
+  (void)out;
+  (void)n;
+  return MYYUV_E_ARG;
+#endif
+}
+
+// Diagnostic builds (-DMYYUV_STAMPS): K2's per-wave window phases of the last
+// launch, n waves x 8 words (k_huff_encode.hip g_k2_win; word 7 = 1 for a
+// wave that ran), then zeroed.
+int myyuv_debug_k2_win(uint32_t* out, uint32_t n) {
+#ifdef MYYUV_STAMPS
+  if (n > 65536) n = 65536;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_win), (size_t)n * 32) != hipSuccess) return MYYUV_E_HIP;
+  std::vector<uint32_t> zero((size_t)n * 8, 0u);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_k2_win), zero.data(), (size_t)n * 32) == hipSuccess ? 0 : MYYUV_E_HIP;
 #else
   (void)out;
   (void)n;
