@@ -45,10 +45,10 @@ kms, kn = c.kernel_stats()["huff_encode"]
 rc = L.myyuv_debug_k2_win(buf, NW)
 a = np.frombuffer(buf, np.uint32).reshape(NW, 8).astype(np.float64)
 a = a[a[:, 7] > 0]
-names = {5: "words+classify", 0: "scan+sort+barriers", 1: "fetch+load+build", 2: "emit+lists", 4: "last fetch+epilogue"}
-tot = a[:, [0, 1, 2, 4, 5]].sum()
+names = {6: "tiles+block words", 5: "classify", 0: "scan+sort+barriers", 1: "fetch+load+build", 2: "emit+lists", 4: "last fetch+epilogue"}
+tot = a[:, [0, 1, 2, 4, 5, 6]].sum()
 print(f"rc={rc} K2 {kms / kn * 1e3:.1f} us per {B}-frame launch; waves stamped {len(a)} (of the first {NW}), "
       f"runs/wave {a[:, 3].mean():.2f}")
 for i, nm in names.items():
     print(f"  {nm:20s} {a[:, i].mean():9.0f} cycles/wave (p90 {np.percentile(a[:, i], 90):8.0f})  {a[:, i].sum() / tot:6.1%}")
-print(f"  total                {a[:, [0, 1, 2, 4, 5]].sum(1).mean():9.0f} cycles/wave")
+print(f"  total                {a[:, [0, 1, 2, 4, 5, 6]].sum(1).mean():9.0f} cycles/wave")

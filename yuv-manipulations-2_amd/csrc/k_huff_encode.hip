@@ -87,7 +87,8 @@ __device__ uint32_t g_k2_fstamps[8192 * 8];
     }                                                                                \
     _tprev = _t;                                                                     \
   } while (0)
-// K2's window phases per wave: [5] tiles, block words and classification,
+// K2's window phases per wave: [6] tiles and the block words' arrival,
+// [5] classification,
 // [0] the rest of the prologue (count scan, sort, three barriers),
 // [1] runs' fetch + load + build, [2] runs' emission and lists, [3] runs,
 // [4] the last fetch + epilogue, [7] = 1 (g_k2_win[wave][8])
@@ -1076,7 +1077,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   __shared__ WinScratch sc;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 #ifdef MYYUV_STAMPS
-  uint32_t _kw[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+  uint32_t _kw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
   unsigned long long _kwprev = __builtin_amdgcn_s_memtime();
 #endif
   const uint32_t NT = G.nframes * G.tcum[3];
@@ -1115,6 +1116,10 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   uint32_t biv[kWinTiles];
 #pragma unroll
   for (uint32_t k = 0; k < kWinTiles; k++) biv[k] = tid < nlk[k] ? binfo[gbk[k] + tid] : 0u;
+#ifdef MYYUV_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (diagnostic: the block words' arrival)
+  KWSTAMP(6);
+#endif
 #pragma unroll
   for (uint32_t k = 0; k < kWinTiles; k++) {
     const uint32_t bi = biv[k];
@@ -1122,13 +1127,23 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     const uint32_t m = (bi >> 8) & 127u, rm = bi & 0xFFu;
     const uint32_t key = sort_key(cls, m);
     sc.dc[(k << 8) | tid] = (uint16_t)(bi >> 18);  // the DC's low 11 bits (build_single_dc uses those)
-    uint32_t rk = 0;
+    // the round's count per key and the lane's rank among its key's lanes
+    // from one ballot per key bit: a lane's equal-key mask is the AND of each
+    // bit's ballot or its complement (lane order: a stable sort), lane c < kKeys
+    // writes key c's count.  No loop over the keys: kKeys ballots, each with
+    // its own exec branch, took 16 % of a wave's cycles (profiles/r5au_k2_phase.txt)
+    static_assert(kKeys <= 16 && kKeys <= 64, "four key bits");
+    uint64_t bb[4];
 #pragma unroll
-    for (uint32_t c = 0; c < kKeys; c++) {
-      const uint64_t b = __ballot(key == c);
-      if (key == c) rk = lanes_below(b);
-      if (lane == 0) sc.cnt[c * kWinRuns + k * kTileWaves + wave] = (uint32_t)__popcll(b);
-    }
+    for (int j = 0; j < 4; j++) bb[j] = __ballot((key >> j) & 1u);
+    auto eq_mask = [&](uint32_t v) {
+      uint64_t e = ~0ull;
+#pragma unroll
+      for (int j = 0; j < 4; j++) e &= ((v >> j) & 1u) ? bb[j] : ~bb[j];
+      return e;
+    };
+    const uint32_t rk = lanes_below(eq_mask(key));
+    if (lane < kKeys) sc.cnt[lane * kWinRuns + k * kTileWaves + wave] = (uint32_t)__popcll(eq_mask(lane));
     ent[k] = cls | (m << 3) | (rm << 10) | (rk << 18) | (key << 24);
   }
 #ifdef MYYUV_STAMPS
@@ -1270,7 +1285,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   KWSTAMP(4);
   {
     const uint32_t wid = blockIdx.x * (kK2Group / kWave) + wave;
-    if (lane < 8 && wid < 65536) g_k2_win[wid * 8 + lane] = lane < 6 ? _kw[lane < 6 ? lane : 0] : (lane == 7 ? 1u : 0u);
+    if (lane < 8 && wid < 65536) g_k2_win[wid * 8 + lane] = lane < 7 ? _kw[lane < 7 ? lane : 0] : 1u;
   }
 #endif
 }
