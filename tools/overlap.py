@@ -5,8 +5,14 @@ per kernel the summed busy time, and over the densest window of codec
 launches the time with k kernels running at once (k = 0, 1, 2, ...)."""
 import collections
 import csv
+import re
 import sys
 
+
+
+def kname(n):
+    """Short kernel name: no namespace, return type or template arguments (k_huff_encode<8u> -> huff_encode)."""
+    return re.sub(r"<[^>]*>$", "", n.split("(")[0].replace("void ", "").replace("myyuv_gpu::k_", ""))
 
 def main(path):
     rows = []
@@ -15,7 +21,7 @@ def main(path):
             n = r["Kernel_Name"]
             if "myyuv_gpu::" not in n:
                 continue
-            k = n.split("(")[0].replace("myyuv_gpu::k_", "").replace("void ", "")
+            k = kname(n)
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
     rows.sort()
     # the timed region: the longest run of launches with gaps < 200 us

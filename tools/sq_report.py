@@ -5,10 +5,16 @@ import collections
 import csv
 import glob
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+
+
+def kname(n):
+    """Short kernel name: no namespace, return type or template arguments (k_huff_encode<8u> -> huff_encode)."""
+    return re.sub(r"<[^>]*>$", "", n.split("(")[0].replace("void ", "").replace("myyuv_gpu::k_", ""))
 
 def main(tag):
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -16,7 +22,7 @@ def main(tag):
         per = collections.defaultdict(float)
         with open(path) as f:
             for r in csv.DictReader(f):
-                k = r["Kernel_Name"].split("(")[0].replace("myyuv_gpu::k_", "")
+                k = kname(r["Kernel_Name"])
                 per[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
         for (k, _, c), v in per.items():
             vals[k][c].append(v)

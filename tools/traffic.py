@@ -17,16 +17,22 @@ import csv
 import json
 import os
 import shutil
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+
+def kname(n):
+    """Short kernel name: no namespace, return type or template arguments (k_huff_encode<8u> -> huff_encode)."""
+    return re.sub(r"<[^>]*>$", "", n.split("(")[0].replace("void ", "").replace("myyuv_gpu::k_", ""))
+
 def per_kernel(path):
     d = collections.defaultdict(list)
     with open(path) as f:
         for r in csv.DictReader(f):
-            d[r["Kernel_Name"].split("(")[0].replace("myyuv_gpu::k_", "")].append(float(r["Counter_Value"]))
+            d[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in d.items()}
 
 
@@ -60,7 +66,7 @@ def main(tag):
     durations = {}
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
-            durations[r["Name"].split("(")[0].replace("myyuv_gpu::k_", "")] = float(r["AverageNs"])
+            durations[kname(r["Name"])] = float(r["AverageNs"])
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"))
     cf, cname = calib_factors()

@@ -205,7 +205,27 @@ __host__ __device__ __forceinline__ uint32_t coef_quad(uint32_t g, uint32_t c) {
 #endif
 constexpr uint32_t kWinTiles = MYYUV_K2_WIN;
 static_assert((kWinTiles & (kWinTiles - 1)) == 0 && kWinTiles >= 1 && kWinTiles <= 8, "kWinTiles: 1, 2, 4 or 8");
-__host__ __device__ __forceinline__ uint32_t win_first_tile(uint32_t T) { return T & ~(kWinTiles - 1u); }
+// Launches of at least kWinBigTiles batch tiles (the bench's 24-frame groups:
+// 26.6k) use windows of kWinTilesBig tiles: twice the runs per workgroup
+// share one classification and sort (bench +1.25 %), while smaller launches
+// (a single 8192x8192 frame: 6,144 tiles) keep kWinTiles, whose grid fills
+// the chip (K2 there 72 against 100 us with 8-tile windows, profiles/r5ba_*).
+// K2 and K4 of one launch use the same window (k2_win), the fused encoder
+// kWinTiles.
+#ifndef MYYUV_K2_WIN_BIG
+#define MYYUV_K2_WIN_BIG 8
+#endif
+#ifndef MYYUV_K2_WIN_BIG_TILES
+#define MYYUV_K2_WIN_BIG_TILES 16384
+#endif
+constexpr uint32_t kWinTilesBig = MYYUV_K2_WIN_BIG;
+constexpr uint32_t kWinBigTiles = MYYUV_K2_WIN_BIG_TILES;
+static_assert((kWinTilesBig & (kWinTilesBig - 1)) == 0 && kWinTilesBig >= kWinTiles && kWinTilesBig <= 8,
+              "kWinTilesBig: a power of two, kWinTiles .. 8");
+__host__ __device__ __forceinline__ uint32_t k2_win(uint32_t ntiles) {
+  return ntiles >= kWinBigTiles ? kWinTilesBig : kWinTiles;
+}
+__host__ __device__ __forceinline__ uint32_t win_first_tile(uint32_t T, uint32_t W) { return T & ~(W - 1u); }
 
 // K2 -> K4 hand-off, per window of batch tiles:
 //   stage:  kTileCap bytes per batch tile (the window's tiles' regions are
@@ -233,7 +253,7 @@ static_assert(1 + kK2Group / kWave <= kTInfoPrefix, "tinfo run words overlap the
 
 // Batch tiles rounded up to whole windows (the stage buffer's extent).
 __host__ __device__ __forceinline__ uint32_t win_tiles_alloc(uint32_t ntiles) {
-  return (ntiles + kWinTiles - 1u) & ~(kWinTiles - 1u);
+  return (ntiles + kWinTilesBig - 1u) & ~(kWinTilesBig - 1u);
 }
 
 // Plane, first block (frame-local) and block count of tile t of a frame.

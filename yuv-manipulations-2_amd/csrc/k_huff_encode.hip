@@ -968,11 +968,10 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
 namespace {
 
 // K2's window sort (k_huff_encode): the window's blocks are counting-sorted
-// by class (dead slots last) over kWinTiles tiles at once.  Sort slots are
-// the (tile round, wave) pairs that classified them, so the order is stable:
-// class, then window slot (tile, block).
-constexpr uint32_t kWinBlocks = kWinTiles * kK2Group;
-constexpr uint32_t kWinRuns = kWinBlocks / kWave;  // 64-block runs per window
+// by class (dead slots last) over the window's W tiles at once (W =
+// kWinTiles or kWinTilesBig, k2_win).  Sort slots are the (tile round, wave)
+// pairs that classified them, so the order is stable: class, then window slot
+// (tile, block).
 // sort keys: the single class, then each of the other classes split by
 // message length (<= 8, <= 16, longer: the per-position loops run to the
 // run's longest message), the dead slots last
@@ -988,8 +987,13 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t cls, uint32_t msz) {
   const uint32_t b = kMszBuckets == 1 ? 0u : (msz > 8 ? 1u : 0u) + (msz > 16 ? 1u : 0u);
   return 1 + (cls - 1) * kMszBuckets + b;
 }
-constexpr uint32_t kScanVals = kKeys * kWinRuns;  // [key][round * 4 + wave] counts
-constexpr uint32_t kScanPer = (kScanVals + kWave - 1) / kWave;
+template <uint32_t W>
+struct WinCfg {
+  static constexpr uint32_t kBlocks = W * kK2Group;
+  static constexpr uint32_t kRuns = kBlocks / kWave;                   // 64-block runs per window
+  static constexpr uint32_t kScanVals = kKeys * kRuns;                 // [key][round * 4 + wave] counts
+  static constexpr uint32_t kScanPer = (kScanVals + kWave - 1) / kWave;
+};
 static_assert(kK2Group == 256, "window slots are tile << 8 | block");
 
 // set bits of m below the calling lane (v_mbcnt: no 64-bit lane mask held)
@@ -1031,19 +1035,20 @@ __device__ __forceinline__ uint32_t wave_incl_sum_full(uint32_t x) {
   return x;
 }
 
+template <uint32_t W>
 struct WinScratch {
-  uint16_t slot[kWinBlocks];  // sorted position -> window slot (tile << 8 | block)
-  uint16_t dc[kWinBlocks];    // window slot -> its DC coefficient's low 11 bits (from K1's block word)
-  uint8_t msz[kWinBlocks], cls[kWinBlocks], rm[kWinBlocks];
-  uint32_t cnt[kScanVals];    // per (key, sort slot): count, then exclusive position
-  uint32_t gb[kWinTiles];     // batch-global index of tile k's block 0
-  uint32_t tot[kWinTiles];    // tile k's dense chunk bytes
+  uint16_t slot[WinCfg<W>::kBlocks];  // sorted position -> window slot (tile << 8 | block)
+  uint16_t dc[WinCfg<W>::kBlocks];    // window slot -> its DC coefficient's low 11 bits (from K1's block word)
+  uint8_t msz[WinCfg<W>::kBlocks], cls[WinCfg<W>::kBlocks], rm[WinCfg<W>::kBlocks];
+  uint32_t cnt[WinCfg<W>::kScanVals];  // per (key, sort slot): count, then exclusive position
+  uint32_t gb[W];             // batch-global index of tile k's block 0
+  uint32_t tot[W];            // tile k's dense chunk bytes
   uint32_t next, done, ntl;   // run counter, finished waves, the window's tiles
 };
 
 }  // namespace
 
-// K2 over K1's coefficients in HBM: one workgroup per window of kWinTiles
+// K2 over K1's coefficients in HBM: one workgroup per window of W (k2_win)
 // batch tiles (grid: windows).
 //   coef: natural-order quads (codec_common.hpp); sizes: [n] u8.
 // 1. classify: thread i takes block i of each of the window's tiles (one
@@ -1065,6 +1070,7 @@ struct WinScratch {
 #ifndef MYYUV_K2_WAVES
 #define MYYUV_K2_WAVES 5  // 5 workgroups of 4 waves per CU: <= 96 VGPRs (12 spilled; 6 measured +1.5 % before the emit tables, −1 % after: its spills grew; tools/ab_bench.sh, tools/kus_ab.sh)
 #endif
+template <uint32_t W>
 __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const uint4* __restrict__ coef,
                                                          const uint32_t* __restrict__ binfo,
                                                          const uint4* __restrict__ zq, FrameGeom G,
@@ -1074,18 +1080,19 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
                                                          uint32_t* __restrict__ srcoff,
                                                          uint32_t* __restrict__ work,
                                                          uint32_t* __restrict__ work_count) {
-  __shared__ WinScratch sc;
+  constexpr uint32_t kWinRuns = WinCfg<W>::kRuns, kScanVals = WinCfg<W>::kScanVals, kScanPer = WinCfg<W>::kScanPer;
+  __shared__ WinScratch<W> sc;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 #ifdef MYYUV_STAMPS
   uint32_t _kw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
   unsigned long long _kwprev = __builtin_amdgcn_s_memtime();
 #endif
   const uint32_t NT = G.nframes * G.tcum[3];
-  const uint32_t T0 = blockIdx.x * kWinTiles;
+  const uint32_t T0 = blockIdx.x * W;
   // ---- the window's tiles (wave-uniform)
-  uint32_t gbk[kWinTiles], nlk[kWinTiles];
+  uint32_t gbk[W], nlk[W];
 #pragma unroll
-  for (uint32_t k = 0; k < kWinTiles; k++) {
+  for (uint32_t k = 0; k < W; k++) {
     const uint32_t T = T0 + k;
     nlk[k] = 0;
     gbk[k] = 0;
@@ -1098,7 +1105,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
       gbk[k] = f * G.cum[3] + g0;
     }
   }
-  if (tid < kWinTiles) {
+  if (tid < W) {
     sc.gb[tid] = gbk[tid];
     sc.tot[tid] = 0;
     // the overflow passes add their chunk bytes to the tile's info word 0
@@ -1108,20 +1115,20 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   if (tid == 0) {
     sc.next = 0;
     sc.done = 0;
-    sc.ntl = min(kWinTiles, NT - T0);
+    sc.ntl = min(W, NT - T0);
   }
   // ---- 1. classify from K1's per-block words (row mask, msz, class, DC;
   // 4 B per block, coalesced), with per-round ballot ranks
-  uint32_t ent[kWinTiles];  // per round: class | msz << 3 | row mask << 10 | rank << 18
-  uint32_t biv[kWinTiles];
+  uint32_t ent[W];  // per round: class | msz << 3 | row mask << 10 | rank << 18
+  uint32_t biv[W];
 #pragma unroll
-  for (uint32_t k = 0; k < kWinTiles; k++) biv[k] = tid < nlk[k] ? binfo[gbk[k] + tid] : 0u;
+  for (uint32_t k = 0; k < W; k++) biv[k] = tid < nlk[k] ? binfo[gbk[k] + tid] : 0u;
 #ifdef MYYUV_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (diagnostic: the block words' arrival)
   KWSTAMP(6);
 #endif
 #pragma unroll
-  for (uint32_t k = 0; k < kWinTiles; k++) {
+  for (uint32_t k = 0; k < W; k++) {
     const uint32_t bi = biv[k];
     const uint32_t cls = tid < nlk[k] ? (bi >> 15) & 7u : kClassDead;
     const uint32_t m = (bi >> 8) & 127u, rm = bi & 0xFFu;
@@ -1170,7 +1177,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t k = 0; k < kWinTiles; k++) {
+  for (uint32_t k = 0; k < W; k++) {
     const uint32_t x = ent[k];
     const uint32_t pos = sc.cnt[(x >> 24) * kWinRuns + k * kTileWaves + wave] + ((x >> 18) & 63u);
     sc.slot[pos] = (uint16_t)((k << 8) | tid);
@@ -1246,7 +1253,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     const uint32_t nhdr = (uint32_t)__builtin_amdgcn_ds_bpermute(nl << 2, (int)(dense ? S.hdr : 0u));
     if (dense) {
       DenseWriter dw;
-      dw.init(stage + ((size_t)blockIdx.x * kWinTiles * (kTileCap / 4) + run * (kWaveRun / 4)), off);
+      dw.init(stage + ((size_t)blockIdx.x * W * (kTileCap / 4) + run * (kWaveRun / 4)), off);
       emit_chunk(S, wmsz, dw);
       dw.finish(above ? (nhdr | 0x80000000u) : 0u);
       sizes[mg] = (uint8_t)S.size;
@@ -1274,7 +1281,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   if (d == kTileWaves - 1) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (lane < sc.ntl) {
-      uint32_t* info = tinfo + (size_t)(blockIdx.x * kWinTiles + lane) * kTInfoWords;
+      uint32_t* info = tinfo + (size_t)(blockIdx.x * W + lane) * kTInfoWords;
       info[1] = __hip_atomic_load(&sc.tot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       info[2] = 0u;
       info[3] = 0u;
@@ -1499,5 +1506,17 @@ __global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const u
     }
   }
 }
+
+
+// the two window sizes (k2_win)
+#define MYYUV_K2_INST(W)                                                                                         \
+  template __global__ void k_huff_encode<W>(const uint4* __restrict__, const uint32_t* __restrict__,             \
+                                            const uint4* __restrict__, FrameGeom, uint32_t* __restrict__,       \
+                                            uint32_t* __restrict__, uint8_t* __restrict__, uint32_t* __restrict__, \
+                                            uint32_t* __restrict__, uint32_t* __restrict__);
+MYYUV_K2_INST(kWinTiles)
+#if MYYUV_K2_WIN_BIG != MYYUV_K2_WIN
+MYYUV_K2_INST(kWinTilesBig)
+#endif
 
 }  // namespace myyuv_gpu

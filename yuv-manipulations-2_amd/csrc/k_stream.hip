@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
                                                     const uint8_t* __restrict__ sizes,
                                                     const uint32_t* __restrict__ srcoff,
                                                     const uint32_t* __restrict__ oslots, FrameGeom G,
-                                                    uint8_t* __restrict__ out, uint32_t cap) {
+                                                    uint8_t* __restrict__ out, uint32_t cap, uint32_t W) {
   __shared__ uint32_t s_wt[4], s_hdr[4];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // the kernel arguments this workgroup uses, consumed at once (the compiler
@@ -320,14 +320,14 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
   uint32_t ntile = G.tcum[3], nframes = G.nframes, tc1 = G.tcum[1], tc2 = G.tcum[2];
   uint32_t c1 = G.cum[1], c2 = G.cum[2], c3 = G.cum[3];
   asm volatile("" : "+s"(ntile), "+s"(nframes), "+s"(tc1), "+s"(tc2), "+s"(c1), "+s"(c2), "+s"(c3), "+s"(cap),
-               "+s"(stage), "+s"(oslots));
+               "+s"(stage), "+s"(oslots), "+s"(W));
   // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and
   // b + 8 share one L2), and a K2 window's kWinTiles tiles read interleaved
   // pieces of the same stage lines, so they go to one XCD: workgroup L takes
-  // batch tile kWinTiles * (8 * (L / (8 kWinTiles)) + L % 8) + (L / 8) %
-  // kWinTiles (a bijection on the grid, a multiple of 8 * kWinTiles)
-  const uint32_t L = blockIdx.x, slot = L >> 3;
-  const uint32_t T0 = kWinTiles * ((slot / kWinTiles) * 8u + (L & 7u)) + slot % kWinTiles;
+  // batch tile W * (8 * (L / (8 W)) + L % 8) + (L / 8) % W (a bijection on
+  // the grid, a multiple of 8 W; W: the launch's K2 window, k2_win)
+  const uint32_t L = blockIdx.x, slot = L >> 3, wl = (uint32_t)__builtin_ctz(W);
+  const uint32_t T0 = (((slot >> wl) * 8u + (L & 7u)) << wl) + (slot & (W - 1u));
   // a surplus workgroup (the grid is a multiple of 8 * kWinTiles) runs the
   // first round trip on the last tile and returns after it: no branch ahead
   // of the kernel-argument and first loads
@@ -368,12 +368,12 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
     src = oslots + (size_t)(gb + tid) * kSlotWords;
     sh = 0;
   } else {
-    src = stage + (size_t)win_first_tile(T) * (kTileCap / 4) + (so >> 2);  // (window-relative)
+    src = stage + (size_t)win_first_tile(T, W) * (kTileCap / 4) + (so >> 2);  // (window-relative)
     sh = so & 3u;
   }
   const uint32_t* s1 = plane_end ? stage
                        : so1 == kSrcOverflow ? oslots + (size_t)(gb + nloc) * kSlotWords
-                                             : stage + (size_t)win_first_tile(T + 1) * (kTileCap / 4) + (so1 >> 2);
+                                             : stage + (size_t)win_first_tile(T + 1, W) * (kTileCap / 4) + (so1 >> 2);
   const uint32_t r1 = plane_end || so1 == kSrcOverflow ? 0u : so1 & 3u;
   // Round trip 2: the chunk's first kVw source words (every chunk of the
   // bench frame: its longest is 55 bytes; predicated per word: most chunks

@@ -37,6 +37,7 @@ __global__ void k_dequant_idct(const uint4*, const uint8_t*, const uint4*, Frame
 __global__ void k_decode_idct(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*, const uint32_t*,
                               const uint32_t*, FrameGeom, uint32_t, uint32_t, const QTables*, uint4*, uint8_t*,
                               unsigned long long*);
+template <uint32_t W>
 __global__ void k_huff_encode(const uint4*, const uint32_t*, const uint4*, FrameGeom, uint32_t*, uint32_t*,
                               uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_huff_encode_wave(const uint4*, const uint8_t*, FrameGeom, uint32_t*, uint8_t*, uint32_t*,
@@ -54,7 +55,7 @@ __global__ void k_scan_chain(const uint8_t*, uint32_t, ScanSrc, const uint32_t*,
                              StreamDesc*, uint32_t*, uint32_t*, uint32_t, unsigned long long*,
                              uint32_t, unsigned long long*);
 __global__ void k_stream_out(const uint32_t*, const uint32_t*, const uint8_t*, const uint32_t*,
-                             const uint32_t*, FrameGeom, uint8_t*, uint32_t);
+                             const uint32_t*, FrameGeom, uint8_t*, uint32_t, uint32_t);
 __global__ void k_huff_decode(const uint8_t*, const uint32_t*, uint32_t, const StreamDesc*,
                               const uint32_t*, const uint32_t*, FrameGeom, uint32_t, uint32_t,
                               uint4*, uint8_t*, unsigned long long*);
@@ -400,7 +401,10 @@ int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   uint32_t* count = c->work.as<uint32_t>();
   uint32_t* list = count + 64;
   // (*count was zeroed by K1, just before in the stream: k_fdct_quant's k2ctl)
-  const int e = launch(c, MYYUV_K_HUFF_ENC, k_huff_encode, dim3(win_tiles_alloc(nf * G.tcum[3]) / kWinTiles), dim3(kK2Group), s,
+  // (the window size of the launch, k2_win: K4 uses the same)
+  const uint32_t W = k2_win(nf * G.tcum[3]);
+  const int e = launch(c, MYYUV_K_HUFF_ENC, W == kWinTilesBig ? k_huff_encode<kWinTilesBig> : k_huff_encode<kWinTiles>,
+                       dim3(win_tiles_alloc(nf * G.tcum[3]) / W), dim3(kK2Group), s,
                c->coef.as<const uint4>(), c->binfo.as<const uint32_t>(), c->zq.as<const uint4>(), G,
                c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
                c->srcoff.as<uint32_t>(), list, count);
@@ -498,10 +502,12 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
   }
   e |= launch(c, MYYUV_K_SCAN, k_tile_scan, dim3(nf), dim3(256), s, c->tinfo.as<uint32_t>(), G,
               static_cast<uint8_t*>(d_out), cap, d_size, err);
-  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(ceil_div(G.tcum[3] * nf, 8 * kWinTiles) * 8 * kWinTiles), dim3(256), s,
+  // K4 reads the stage in K2's windows (k2_win; the fused encoder's: kWinTiles)
+  const uint32_t W = c->fused ? kWinTiles : k2_win(nf * G.tcum[3]);
+  e |= launch(c, MYYUV_K_COMPACT, k_stream_out, dim3(ceil_div(G.tcum[3] * nf, 8 * W) * 8 * W), dim3(256), s,
               c->stage.as<const uint32_t>(), c->tinfo.as<const uint32_t>(), c->sizes.as<const uint8_t>(),
               c->srcoff.as<const uint32_t>(), c->oslots.as<const uint32_t>(), G, static_cast<uint8_t*>(d_out),
-              cap);
+              cap, W);
   return e ? MYYUV_E_HIP : 0;
 }
 
@@ -1232,7 +1238,7 @@ int myyuv_gpu_huff_encode_blocks(myyuv_hip_handle c, const int16_t* coef_zz, uin
     uint8_t* dst = chunks160 + (size_t)g * kMaxChunk;
     std::memset(dst, 0, kMaxChunk);
     const uint8_t* src = soff[g] == kSrcOverflow ? oslots.data() + (size_t)g * kMaxChunk
-                                                 : stage.data() + (size_t)win_first_tile(g / kK2Group) * kTileCap + soff[g];
+                                                 : stage.data() + (size_t)win_first_tile(g / kK2Group, k2_win(G.nframes * ntile)) * kTileCap + soff[g];
     std::memcpy(dst, src, sizes[g]);
   }
   return 0;
