@@ -371,6 +371,42 @@ def test_batch_device_matches_single_frames(codec, oracle, golden, wh, n, q):
             assert bytes(out[f * fb:(f + 1) * fb]) == oracle.decompress(exp, w, h, q), f
 
 
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_k2_windows_stay_inside_the_tiles(codec, oracle, chef_big, n):
+    """Round 5's advice: with 4-tile K2 windows and a tile count of 1, 2 or 3
+    mod 8 (chef-big: 1,113 tiles per frame), K2's grid once had a window past
+    the last tile, which wrote tile-info words beyond the buffer.  A canary
+    band after the batch's last tile must survive the compression, and the
+    streams must stay the pinned / oracle bytes."""
+    import torch
+    import myyuv_hip
+    f, raw = chef_big
+    w, h, q = f.width, f.height, (50, 50, 50)
+    nt = n * myyuv_hip.batch_tiles(w, h)
+    assert nt % 8 == n  # the regime the advice names
+    fb = w * h * 3 // 2
+    cap = (myyuv_hip.payload_bound(w, h) + 3) & ~3
+    d_in = torch.frombuffer(bytearray(raw * n), dtype=torch.uint8).cuda()
+    d_pay = torch.zeros(n * cap, dtype=torch.uint8, device="cuda")
+    d_sizes = torch.zeros(n, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    codec.reserve_batch(w, h, n)
+    codec.tinfo_guard(nt, True)
+    codec.compress_batch_device(d_in.data_ptr(), n, w, h, q, d_pay.data_ptr(), cap, d_sizes.data_ptr(), stream)
+    rc, bad = codec.sync_status(stream)
+    assert rc == 0, (rc, bad)
+    assert codec.tinfo_guard(nt, False) == 0
+    pay = d_pay.cpu().numpy()
+    sizes = d_sizes.cpu().numpy()
+    for i in range(n):
+        got = bytes(pay[i * cap: i * cap + int(sizes[i])])
+        assert sha(got) == "fe9b7317653c2b44a9f24436f0e349b083b4e368cf9653e8777e9f7a79cebfcc", i
+    if n == 1:  # the host-buffer entry point too
+        codec.tinfo_guard(nt, True)
+        assert sha(codec.compress(raw, w, h, q)) == "fe9b7317653c2b44a9f24436f0e349b083b4e368cf9653e8777e9f7a79cebfcc"
+        assert codec.tinfo_guard(nt, False) == 0
+
+
 def test_batch_decode_error_reports_frame(codec, oracle, golden):
     """A malformed chunk in frame 1 of a batch: the reference's error, at the
     batch-global index of the failing block (frame 1 * blocks per frame + block)."""

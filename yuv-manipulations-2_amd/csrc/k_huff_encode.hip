@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
   if (tid == 0) {
     sc.next = 0;
     sc.done = 0;
-    sc.ntl = min(W, NT - T0);
+    sc.ntl = T0 < NT ? min(W, NT - T0) : 0u;  // (no window starts past the end: grid ceil(NT / W))
   }
   // ---- 1. classify from K1's per-block words (row mask, msz, class, DC;
   // 4 B per block, coalesced), with per-round ballot ranks

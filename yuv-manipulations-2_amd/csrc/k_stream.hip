@@ -322,13 +322,13 @@ __global__ __launch_bounds__(256) void k_stream_out(const uint32_t* __restrict__
   asm volatile("" : "+s"(ntile), "+s"(nframes), "+s"(tc1), "+s"(tc2), "+s"(c1), "+s"(c2), "+s"(c3), "+s"(cap),
                "+s"(stage), "+s"(oslots), "+s"(W));
   // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and
-  // b + 8 share one L2), and a K2 window's kWinTiles tiles read interleaved
+  // b + 8 share one L2), and a K2 window's W tiles read interleaved
   // pieces of the same stage lines, so they go to one XCD: workgroup L takes
   // batch tile W * (8 * (L / (8 W)) + L % 8) + (L / 8) % W (a bijection on
   // the grid, a multiple of 8 W; W: the launch's K2 window, k2_win)
   const uint32_t L = blockIdx.x, slot = L >> 3, wl = (uint32_t)__builtin_ctz(W);
   const uint32_t T0 = (((slot >> wl) * 8u + (L & 7u)) << wl) + (slot & (W - 1u));
-  // a surplus workgroup (the grid is a multiple of 8 * kWinTiles) runs the
+  // a surplus workgroup (the grid is a multiple of 8 * W) runs the
   // first round trip on the last tile and returns after it: no branch ahead
   // of the kernel-argument and first loads
   const bool surplus = T0 >= ntile * nframes;

@@ -37,12 +37,22 @@
 // A launch covers a batch of frames (FrameGeom::nframes): the waves stride
 // over the units of all of them, frame f's unit u being f * ucum[3] + u.
 //
-// Bit-exactness (SURVEY.md §7 hard part 1, App. C): each output is the
-// reference's straight k-ascending sum of fp32-rounded products
-// (DCT.cpp:232-266; stage 1 accumulates row k at a time, which is still
-// k-ascending for every output); -ffp-contract=off keeps products and sums
-// separately rounded (the only fma is the explicit near-tie test).
-//   K1 /Q + roundf: t = y * fl(1/Q) is within |t| * 1.5 * 2^-23 of fl(y/Q)
+// Bit-exactness (SURVEY.md §7 hard part 1, App. C).  K1's fast path
+// (fdct_fast, xform_common.hpp) is an even/odd BUTTERFLY over a nominal
+// basis N (the literal DCT_matrix8 of DCT.cpp:221-230 made exactly symmetric,
+// fdct_bfly.h): it does not reproduce the reference's operation order, so
+// each 16-block unit carries a proof instead.  With A = sum |x - 128| over the
+// block, |Y_fast - Y_ref| <= kappa * A (Higham gamma_k bounds on both
+// evaluations plus max|N - D|; fdct_bfly.h), and a row whose every
+// t = Y_fast * fl(1/Q) stays further than A * kb[row] from a half-integer
+// quantises to the reference's roundf(fl(Y_ref / Q)).  A unit where any row
+// fails is listed and recomputed by k_fdct_fix in the reference's order: the
+// straight k-ascending sums of fp32-rounded products (DCT.cpp:232-266),
+// -ffp-contract=off (fdct_exact; its only fma is the near-tie test below).
+// tools/diag/fdct_bfly_check.cpp (tests/test_numerics.py) replays the fast
+// arithmetic on the host and checks every proven unit equals the reference.
+// K6 keeps the reference's order throughout.
+//   exact path /Q + roundf: t = y * fl(1/Q) is within |t| * 1.5 * 2^-23 of fl(y/Q)
 //     (two roundings of relative error 2^-24 plus fl(y/Q)'s own), so
 //     roundf(fl(y/Q)) == rint(t) unless a half-integer lies within
 //     |t| * 2^-21 of t.  rint(t) comes from u = t + 1.5*2^23 (|t| < 2^22:
@@ -62,7 +72,8 @@
 //     has a fractional part of exactly 0.5), where roundf goes away from zero,
 //     differ, and the lane redoes those with truncf(x + copysignf(0.49999997f,
 //     x)) == roundf(x) (exhaustively checked for all 2^32 floats).
-// No butterflies and no MFMA (an MFMA f32 product is an fma chain).
+// No MFMA: this is not a dense contraction, and the bound above admits only
+// evaluations whose every operation rounds once to nearest.
 #include <stddef.h>
 
 #include "codec_common.hpp"

@@ -342,7 +342,9 @@ int reserve(myyuv_hip_ctx* c, const FrameGeom& G) {
   e |= c->coef.grow((size_t)nwaves * kCoefQuadsPerWave * 16);  // natural-order quads
   e |= c->stage.grow((size_t)win_tiles_alloc(nf * G.tcum[3]) * kTileCap);
   e |= c->oslots.grow((size_t)nblk * kMaxChunk);
-  e |= c->tinfo.grow((size_t)nf * G.tcum[3] * kTInfoWords * 4);
+  // (plus a guard band of one big window's tiles past the launch's last tile:
+  // myyuv_debug_tinfo_guard checks that no kernel writes into it)
+  e |= c->tinfo.grow((size_t)(nf * G.tcum[3] + kWinTilesBig) * kTInfoWords * 4);
   e |= c->srcoff.grow((size_t)nblk * 4);
   e |= c->sizes.grow((size_t)nwaves * kWave);
   e |= c->rmask.grow((size_t)nblk);
@@ -404,7 +406,7 @@ int launch_huff_encode(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   // (the window size of the launch, k2_win: K4 uses the same)
   const uint32_t W = k2_win(nf * G.tcum[3]);
   const int e = launch(c, MYYUV_K_HUFF_ENC, W == kWinTilesBig ? k_huff_encode<kWinTilesBig> : k_huff_encode<kWinTiles>,
-                       dim3(win_tiles_alloc(nf * G.tcum[3]) / W), dim3(kK2Group), s,
+                       dim3(ceil_div(nf * G.tcum[3], W)), dim3(kK2Group), s,
                c->coef.as<const uint4>(), c->binfo.as<const uint32_t>(), c->zq.as<const uint4>(), G,
                c->stage.as<uint32_t>(), c->tinfo.as<uint32_t>(), c->sizes.as<uint8_t>(),
                c->srcoff.as<uint32_t>(), list, count);
@@ -1123,6 +1125,30 @@ int myyuv_debug_coef(myyuv_hip_handle c, int16_t* out, uint32_t n) {
       else
         std::memset(out + (size_t)b * 64 + q * 8, 0, 16);
     }
+  return 0;
+}
+
+// Diagnostic: the tile-info guard band.  arm != 0 fills the kWinTilesBig x
+// kTInfoWords words after tile ntiles (the batch's last tile) with a canary;
+// arm == 0 returns in *changed how many of them no longer hold it (a kernel
+// wrote past the batch's tiles: the K2 window overrun of round 5's advice).
+int myyuv_debug_tinfo_guard(myyuv_hip_handle c, uint32_t ntiles, int arm, uint32_t* changed) {
+  if (!c) return MYYUV_E_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  constexpr uint32_t kGuardWords = kWinTilesBig * kTInfoWords;
+  constexpr uint32_t kCanary = 0xA5C3E1F7u;
+  const size_t off = (size_t)ntiles * kTInfoWords * 4;
+  if (off + kGuardWords * 4 > c->tinfo.n) return MYYUV_E_ARG;
+  std::vector<uint32_t> w(kGuardWords, kCanary);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return MYYUV_E_HIP;
+  uint8_t* p = static_cast<uint8_t*>(c->tinfo.p) + off;
+  if (arm) return hipMemcpy(p, w.data(), kGuardWords * 4, hipMemcpyHostToDevice) == hipSuccess ? 0 : MYYUV_E_HIP;
+  if (!changed) return MYYUV_E_ARG;
+  if (hipMemcpy(w.data(), p, kGuardWords * 4, hipMemcpyDeviceToHost) != hipSuccess) return MYYUV_E_HIP;
+  uint32_t n = 0;
+  for (uint32_t v : w) n += v != kCanary;
+  *changed = n;
   return 0;
 }
 

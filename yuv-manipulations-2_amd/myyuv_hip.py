@@ -103,6 +103,7 @@ def load():
     L.myyuv_gpu_bmp_to_iyuv.argtypes = [vp, u8p, i32, i32, ctypes.c_uint16, u8p]
     L.myyuv_gpu_bmp_to_iyuv_device.argtypes = [vp, vp, i32, i32, ctypes.c_uint16, vp, vp]
     L.myyuv_gpu_dct_compress_batch.argtypes = [vp, u8p, u32, u32, u32, u8p, u8p, u32, ctypes.POINTER(u32)]
+    L.myyuv_debug_tinfo_guard.argtypes = [vp, u32, ctypes.c_int, ctypes.POINTER(u32)]  # diagnostic
     _lib = L
     return L
 
@@ -113,6 +114,14 @@ def strerror(code):
 
 def payload_bound(w, h):
     return load().myyuv_dct_payload_bound(w, h)
+
+
+def batch_tiles(w, h):
+    """K2's 256-block tiles per frame (FrameGeom::tcum[3]): per plane
+    ceil(blocks / 256), Y then U and V."""
+    y = (w // 8) * (h // 8)
+    c = (w // 16) * (h // 16)
+    return -(-y // 256) + 2 * -(-c // 256)
 
 
 def _u8(a):
@@ -309,6 +318,16 @@ class Codec:
         if rc:
             raise CodecError(rc)
         return {KERNELS[i]: (ms[i], n[i]) for i in range(len(KERNELS))}
+
+    def tinfo_guard(self, ntiles, arm):
+        """Diagnostic (not in include/myyuv_hip.h): arm=True writes a canary
+        into the tile-info words past batch tile ntiles; arm=False returns how
+        many of them a kernel overwrote since."""
+        n = ctypes.c_uint32(0)
+        rc = load().myyuv_debug_tinfo_guard(self._h, int(ntiles), 1 if arm else 0, ctypes.byref(n))
+        if rc:
+            raise CodecError(rc)
+        return n.value
 
     # -- block-level known-answer entry points --
     def fdct_blocks(self, px, qtable):
