@@ -161,6 +161,8 @@ def parse(argv=None):
                     help="skip the side measurements (decode-only, K7 roofline, host API, batch4k at N=1)")
     ap.add_argument("--host-api-iters", type=int, default=20,
                     help="round trips of the host-buffer API side measurement (0 disables it)")
+    ap.add_argument("--host-batch-frames", type=int, default=32,
+                    help="frames of the pipelined host-buffer batch side measurement (0 disables it)")
     ap.add_argument("--breakdown-steps", type=int, default=5,
                     help="untimed launch groups after the timed region with every kernel stamped")
     ap.add_argument("--input-frames", type=int, default=0,
@@ -867,6 +869,61 @@ def host_api_rate(codec_mod, raw, w, h, q, iters):
         c.close()
 
 
+def host_batch_rate(codec_mod, raw, w, h, q, nframes, reps):
+    """The pipelined host-buffer batches (myyuv_gpu_dct_compress_batch /
+    _decompress_batch: uploads, kernels and downloads of successive chunks
+    overlapped on three streams) over nframes copies of the frame in
+    pageable host buffers allocated once; time = t_compress + t_decompress
+    of the whole batch, median of reps."""
+    import ctypes
+    import numpy as np
+    c = codec_mod.Codec(0)
+    L = codec_mod.load()
+    try:
+        fb = w * h * 3 // 2
+        src = np.tile(np.frombuffer(raw, np.uint8), nframes)
+        cap = (codec_mod.payload_bound(w, h) + 3) & ~3
+        pay = np.zeros(nframes * cap, np.uint8)
+        out = np.zeros(nframes * fb, np.uint8)
+        sizes = (ctypes.c_uint32 * nframes)()
+        qa = np.array([q, q, q], np.uint8)
+        bad = ctypes.c_int64(-1)
+        u8 = codec_mod._u8
+        tc, td = [], []
+        for i in range(reps + 1):
+            t0 = time.perf_counter()
+            rc = L.myyuv_gpu_dct_compress_batch(c._h, u8(src), nframes, w, h, u8(qa), u8(pay), cap, sizes)
+            t1 = time.perf_counter()
+            if rc:
+                raise codec_mod.CodecError(rc)
+            rc = L.myyuv_gpu_dct_decompress_batch(c._h, u8(pay), sizes, cap, nframes, w, h, u8(qa), u8(out),
+                                                  ctypes.byref(bad))
+            t2 = time.perf_counter()
+            if rc:
+                raise codec_mod.CodecError(rc, bad.value)
+            if i >= 1:
+                tc.append(t1 - t0)
+                td.append(t2 - t1)
+        n0 = int(sizes[0])
+        if q == 50 and sha(pay[:n0].tobytes()) != BIG_RECOMPRESSED_SHA:
+            raise SystemExit("host batch: compressed stream differs from the pinned reference bytes")
+        if any(int(sizes[f]) != n0 for f in range(nframes)) or \
+                any(sha(pay[f * cap: f * cap + n0].tobytes()) != sha(pay[:n0].tobytes()) for f in (1, nframes - 1)):
+            raise SystemExit("host batch: frames of one input differ")
+        if out[:fb].tobytes() != raw or out[(nframes - 1) * fb:].tobytes() != raw:
+            raise SystemExit("host batch: decoded frames differ from the input decode")
+        mc, md = statistics.median(tc), statistics.median(td)
+        mp = w * h / 1e6 * nframes
+        pcie = nframes * 2 * (fb + n0)
+        return {"value": round(mp / (mc + md), 1), "unit": "MP/s", "frames": nframes,
+                "compress_ms": round(mc * 1e3, 3), "decompress_ms": round(md * 1e3, 3), "reps": reps,
+                "pcie_bytes": pcie, "pcie_gbs": round(pcie / (mc + md) / 1e9, 2),
+                "api": "myyuv_gpu_dct_compress_batch + myyuv_gpu_dct_decompress_batch (pipelined), "
+                       "pageable host buffers"}
+    finally:
+        c.close()
+
+
 def main(argv=None):
     args = parse(argv)
     rc = maybe_launch(args)
@@ -1085,6 +1142,8 @@ def side_measurements(args, run, codec, raw, big, world, dev):
     del bgra, d_iy
     if args.host_api_iters > 0:
         side["host_api"] = host_api_rate(myyuv_hip, raw, w, h, run.q, args.host_api_iters)
+    if args.host_batch_frames > 0:
+        side["host_batch"] = host_batch_rate(myyuv_hip, raw, w, h, run.q, args.host_batch_frames, 5)
     return side
 
 

@@ -151,15 +151,41 @@ int myyuv_gpu_bmp_to_iyuv(myyuv_hip_handle h, const uint8_t* bmp_data, int32_t w
 int myyuv_gpu_bmp_to_iyuv_device(myyuv_hip_handle h, const void* d_bmp_data, int32_t width,
                                  int32_t height, uint16_t bit_count, void* d_iyuv, void* stream);
 
-/* Host-buffer batch compress (many frames per call):
- * `nframes` IYUV frames of one geometry back to back in `iyuv` (frame f at
- * f*W*H*3/2) -> payload f at payloads + f*cap, its size in sizes[f].  One
- * launch per kernel for the whole batch; every frame's bytes are those of
- * myyuv_gpu_dct_compress.  MYYUV_E_CAPACITY when a payload exceeds `cap`
- * (sizes[] still hold every size). */
+/* Host-buffer batches (many frames per call; §7 step 9:
+ * transfers overlapped with the kernels).  The batch runs in chunks of up to
+ * 8 frames through two device slots: chunk k's host -> device copies, chunk
+ * k-1's kernels (one launch per kernel for the chunk) and chunk k-2's
+ * device -> host copies run at once, on three streams.  Every frame's bytes
+ * are those of the single-frame calls; the calls return when every output
+ * is in host memory.  Replaces a loop of YUV::compress / YUV::decompress
+ * (myyuv_cli/main.cpp:151-207) over many frames.
+ *
+ * Compress: frames[f] -> payload f, written to the buffer alloc(user, f,
+ * size) returns once the frame's size is known (NULL: MYYUV_E_CAPACITY and
+ * the call stops); sizes[f] = its size.  alloc runs on the calling thread,
+ * in frame order. */
+typedef uint8_t* (*myyuv_payload_alloc_fn)(void* user, uint32_t frame, uint32_t size);
+int myyuv_gpu_dct_compress_frames(myyuv_hip_handle h, const uint8_t* const* frames, uint32_t nframes,
+                                  uint32_t width, uint32_t height, const uint8_t quality[3],
+                                  myyuv_payload_alloc_fn alloc, void* user, uint32_t* sizes);
+/* Contiguous form: frame f at iyuv + f*W*H*3/2 -> payload f at payloads +
+ * f*cap.  MYYUV_E_CAPACITY when a payload exceeds `cap` (sizes[] hold the
+ * sizes up to that frame). */
 int myyuv_gpu_dct_compress_batch(myyuv_hip_handle h, const uint8_t* iyuv, uint32_t nframes,
                                  uint32_t width, uint32_t height, const uint8_t quality[3],
                                  uint8_t* payloads, uint32_t cap, uint32_t* sizes);
+/* Decompress: stream f (payloads[f], sizes[f] bytes) -> frames[f]
+ * (W*H*3/2 bytes).  Every stream's header is checked first (the
+ * single-frame call's DCTYUV::load checks); a decode error stops the call
+ * with *bad_block the batch-global index of the failing block (frame f's
+ * block g: f * blocks-per-frame + g). */
+int myyuv_gpu_dct_decompress_frames(myyuv_hip_handle h, const uint8_t* const* payloads, const uint32_t* sizes,
+                                    uint32_t nframes, uint32_t width, uint32_t height, const uint8_t quality[3],
+                                    uint8_t* const* frames, int64_t* bad_block);
+/* Contiguous form: stream f at payloads + f*cap -> frame f at iyuv + f*W*H*3/2. */
+int myyuv_gpu_dct_decompress_batch(myyuv_hip_handle h, const uint8_t* payloads, const uint32_t* sizes,
+                                   uint32_t cap, uint32_t nframes, uint32_t width, uint32_t height,
+                                   const uint8_t quality[3], uint8_t* iyuv, int64_t* bad_block);
 
 /* Waits for `stream`, returns (and clears) the first device-side error since
  * the last call; *bad_block as above. */

@@ -164,11 +164,23 @@ def test_cli_batch_compress_matches_per_file(tmp_path, golden, oracle):
     # and back: -batch-decompress equals -decompress per file
     dec = tmp_path / "dec"
     dec.mkdir()
-    r = run(CLI, "-batch-decompress", "-o", str(dec), str(out / "a.myyuv"), str(out / "c.myyuv"))
+    # (with an uncompressed frame, which -decompress copies, and another quality)
+    q90 = tmp_path / "q90.myyuv"
+    assert run(CLI, str(a), "-compress", "DCT", "90", "-o", str(q90)).returncode == 0
+    ra = tmp_path / "raw_a.myyuv"
+    ra.write_bytes(open(SMALL, "rb").read())
+    r = run(CLI, "-batch-decompress", "-o", str(dec), str(out / "a.myyuv"), str(out / "c.myyuv"), str(ra),
+            str(q90), str(out / "b.myyuv"))
     assert r.returncode == 0, r.stdout + r.stderr
+    assert "(5 frames)" in r.stdout
     one_d = tmp_path / "c1d.myyuv"
     assert run(CLI, str(one), "-decompress", "-o", str(one_d)).returncode == 0
     assert (dec / "c.myyuv").read_bytes() == one_d.read_bytes()
+    for src, name in ((ra, "raw_a.myyuv"), (q90, "q90.myyuv")):
+        per_file = tmp_path / ("d_" + name)
+        assert run(CLI, str(src), "-decompress", "-o", str(per_file)).returncode == 0
+        assert (dec / name).read_bytes() == per_file.read_bytes(), name
+    assert (dec / "b.myyuv").read_bytes() == (dec / "a.myyuv").read_bytes()
     want = myyuv_file.YUVFile.load(gold)
     assert myyuv_file.YUVFile.load(str(dec / "a.myyuv")).data == oracle.decompress(want.data, 992, 736, (50, 50, 50))
 

@@ -231,7 +231,9 @@ int run_batch(const std::vector<std::string>& args) {
       for (const auto& y : in) ptrs.push_back(&y);
       out = myyuvDCT::compress_DCT_planar_batch(ptrs, {q[0], q[1], q[2]}, devices);
     } else {
-      for (const auto& y : in) out.push_back(y.decompress());
+      std::vector<const myyuv::YUV*> ptrs;
+      for (const auto& y : in) ptrs.push_back(&y);
+      out = myyuvDCT::decompress_DCT_planar_batch(ptrs);
     }
   });
   std::cout << (comp ? "YUV DCT batch compression" : "YUV DCT batch decompression") << " (" << in.size()

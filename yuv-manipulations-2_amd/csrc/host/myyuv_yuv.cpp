@@ -331,40 +331,53 @@ myyuv::YUV compress_DCT_planar(const myyuv::YUV& yuv, const std::array<uint8_t, 
 namespace {
 
 // Frames `idx` of `frames` (any geometries) on context h: frames of one
-// geometry share one batched launch of every kernel (up to kMaxBatch).
+// geometry go through one pipelined host batch (myyuv_gpu_dct_compress_frames:
+// uploads, kernels and downloads overlapped, one launch per kernel per chunk);
+// each payload lands in its YUV's own new[] buffer, sized once its length is
+// known.
+struct PayloadSink {
+  std::vector<myyuv::YUV>* out;
+  const std::vector<size_t>* dst;  // batch frame -> index into *out
+};
+uint8_t* payload_sink(void* user, uint32_t frame, uint32_t size) {
+  auto* ps = static_cast<PayloadSink*>(user);
+  myyuv::YUV& res = (*ps->out)[(*ps->dst)[frame]];
+  delete[] res.data;
+  res.data = new uint8_t[size ? size : 1];
+  return res.data;
+}
+
 void compress_share(myyuv_hip_handle h, const std::vector<const myyuv::YUV*>& frames,
                     const std::vector<size_t>& idx, const std::array<uint8_t, 3>& params,
                     std::vector<myyuv::YUV>& out) {
   using myyuv::YUV;
   std::vector<bool> done(idx.size(), false);
-  constexpr size_t kMaxBatch = 16;  // frames per batched launch
   for (size_t i = 0; i < idx.size(); i++) {
     if (done[i]) continue;
     const uint32_t w = frames[idx[i]]->header.width, hh = frames[idx[i]]->header.height;
-    std::vector<size_t> group;  // positions in idx of this geometry, in input order
-    for (size_t j = i; j < idx.size() && group.size() < kMaxBatch; j++)
-      if (!done[j] && frames[idx[j]]->header.width == w && frames[idx[j]]->header.height == hh) group.push_back(j);
-    const size_t fbytes = (size_t)w * hh * 3 / 2;
-    const uint32_t cap = (myyuv_dct_payload_bound(w, hh) + 3u) & ~3u;
-    std::vector<uint8_t> in(fbytes * group.size()), pay((size_t)cap * group.size());
-    std::vector<uint32_t> sizes(group.size());
-    for (size_t k = 0; k < group.size(); k++) std::memcpy(in.data() + k * fbytes, frames[idx[group[k]]]->data, fbytes);
-    const int rc = myyuv_gpu_dct_compress_batch(h, in.data(), (uint32_t)group.size(), w, hh, params.data(),
-                                                pay.data(), cap, sizes.data());
+    std::vector<size_t> dst;  // indices (into frames / out) of this geometry, in input order
+    std::vector<const uint8_t*> src;
+    for (size_t j = i; j < idx.size(); j++)
+      if (!done[j] && frames[idx[j]]->header.width == w && frames[idx[j]]->header.height == hh) {
+        dst.push_back(idx[j]);
+        src.push_back(frames[idx[j]]->data);
+        done[j] = true;
+      }
+    std::vector<uint32_t> sizes(dst.size());
+    PayloadSink ps{&out, &dst};
+    const int rc = myyuv_gpu_dct_compress_frames(h, src.data(), (uint32_t)src.size(), w, hh, params.data(),
+                                                 payload_sink, &ps, sizes.data());
     if (rc) fail(rc);
-    for (size_t k = 0; k < group.size(); k++) {
-      const YUV& src = *frames[idx[group[k]]];
-      YUV& res = out[idx[group[k]]];
-      res.header = src.header;  // header rewrite as compress_DCT_planar (DCT.cpp:389-396)
+    for (size_t k = 0; k < dst.size(); k++) {
+      const YUV& in = *frames[dst[k]];
+      YUV& res = out[dst[k]];
+      res.header = in.header;  // header rewrite as compress_DCT_planar (DCT.cpp:389-396)
       res.header.compression = YUV::Compressions::DCT;
       res.header.compression_params_size = 3;
       res.header.compression_params_pos = sizeof(myyuv::YUVHeader);
       res.header.data_pos = sizeof(myyuv::YUVHeader) + 3;
       res.header.data_size = sizes[k];
       res.compression_params = new uint8_t[3]{params[0], params[1], params[2]};
-      res.data = new uint8_t[sizes[k]];
-      std::memcpy(res.data, pay.data() + k * cap, sizes[k]);
-      done[group[k]] = true;
     }
   }
 }
@@ -447,6 +460,67 @@ myyuv::YUV decompress_DCT_planar(const myyuv::YUV& yuv, const std::array<uint8_t
                                           yuv.header.height, params.data(), res.data, &bad);
   if (rc) fail(rc);
   return res;
+}
+
+
+// Many compressed frames per call.  Each frame is checked as YUV::decompress
+// -> decompress_map[DCT][IYUV] -> decompress_DCT_planar would, in input order
+// (frames that are not DCT / IYUV, or fail a check, take that single-frame
+// path and its error); the DCT frames of one geometry and quality triple
+// then go through one pipelined host batch (myyuv_gpu_dct_decompress_frames)
+// straight into their results' planes.
+std::vector<myyuv::YUV> decompress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames) {
+  using myyuv::YUV;
+  std::vector<YUV> out(frames.size());
+  std::vector<size_t> todo;
+  for (size_t i = 0; i < frames.size(); i++) {
+    const YUV& y = *frames[i];
+    bool batchable = y.getCompression() == YUV::Compressions::DCT && y.getFourccFormat() == YUV::FourccFormats::IYUV &&
+                     y.header.compression_params_size == 3 && y.compression_params &&
+                     y.getFormatGroup() == YUV::FormatGroup::PLANAR;
+    for (int p = 0; batchable && p < 3; p++) batchable = y.compression_params[p] >= 1 && y.compression_params[p] <= 100;
+    if (batchable)
+      todo.push_back(i);
+    else
+      out[i] = y.decompress();
+  }
+  std::vector<bool> done(todo.size(), false);
+  for (size_t i = 0; i < todo.size(); i++) {
+    if (done[i]) continue;
+    const YUV& y0 = *frames[todo[i]];
+    const uint32_t w = y0.header.width, hh = y0.header.height;
+    const uint8_t* q = y0.compression_params;
+    std::vector<size_t> grp;
+    for (size_t j = i; j < todo.size(); j++) {
+      const YUV& y = *frames[todo[j]];
+      if (!done[j] && y.header.width == w && y.header.height == hh && std::memcmp(y.compression_params, q, 3) == 0) {
+        grp.push_back(todo[j]);
+        done[j] = true;
+      }
+    }
+    std::vector<const uint8_t*> src;
+    std::vector<uint32_t> sizes;
+    std::vector<uint8_t*> dstp;
+    for (size_t k : grp) {
+      const YUV& y = *frames[k];
+      YUV& res = out[k];  // header rewrite as decompress_DCT_planar (DCT.cpp:446-453)
+      res.header = y.header;
+      res.header.compression = YUV::Compressions::NONE;
+      res.header.compression_params_size = 0;
+      res.header.compression_params_pos = 0;
+      res.header.data_pos = sizeof(myyuv::YUVHeader);
+      res.header.data_size = res.getImageSize();
+      res.data = new uint8_t[res.header.data_size];
+      src.push_back(y.data);
+      sizes.push_back(y.header.data_size);
+      dstp.push_back(res.data);
+    }
+    int64_t bad = -1;
+    const int rc = myyuv_gpu_dct_decompress_frames(t_codec.get(), src.data(), sizes.data(), (uint32_t)grp.size(), w,
+                                                   hh, q, dstp.data(), &bad);
+    if (rc) fail(rc);
+  }
+  return out;
 }
 
 }  // namespace myyuvDCT

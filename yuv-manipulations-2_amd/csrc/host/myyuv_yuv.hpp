@@ -116,4 +116,7 @@ std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv:
 std::vector<myyuv::YUV> compress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames,
                                                   const std::array<uint8_t, 3>& params,
                                                   const std::vector<int>& devices);
+// Many compressed frames per call: result i is frames[i]->decompress(); the
+// DCT frames of one geometry and quality go through one pipelined host batch.
+std::vector<myyuv::YUV> decompress_DCT_planar_batch(const std::vector<const myyuv::YUV*>& frames);
 }  // namespace myyuvDCT

@@ -232,6 +232,13 @@ struct myyuv_hip_ctx {
   int64_t launches[MYYUV_K_COUNT] = {};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> free_events;
+  // host-buffer batch pipeline (HostPipe below): H2D on cin, kernels on
+  // `stream`, D2H on cout; two slots of up to kPipeMaxChunk frames
+  hipStream_t cin = nullptr, cout = nullptr;
+  hipEvent_t pev[3][2] = {};  // [copied in, computed, copied out][slot]
+  DevBuf pin[2], pout[2], psz[2], perr[2];
+  uint32_t* hsz = nullptr;            // pinned: 2 x kPipeMaxChunk u32 sizes
+  unsigned long long* herr = nullptr;  // pinned: 2 error words
   std::mutex mu;
 };
 
@@ -482,10 +489,10 @@ int launch_fdct(myyuv_hip_ctx* c, const FrameGeom& G, const uint8_t* in, const Q
 // One batch of G.nframes frames (frame f at d_in + f * fbytes), payload f at
 // d_out + f * cap, its size at d_size[f].
 int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void* d_out,
-                    uint32_t cap, uint32_t* d_size, hipStream_t s) {
+                    uint32_t cap, uint32_t* d_size, hipStream_t s, unsigned long long* err = nullptr) {
   const uint32_t nf = G.nframes;
   const QTables* qt = c->qtd.as<const QTables>();
-  unsigned long long* err = c->err.as<unsigned long long>();
+  if (!err) err = c->err.as<unsigned long long>();
   int e = 0;
   if (c->fused) {
     // fused single-pass encoder (K1 + K2 per tile), then the overflow passes
@@ -516,12 +523,13 @@ int launch_compress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in, void
 // The mirror: payload f at d_in + f * cap (size d_size[f]) -> frame f at
 // d_out + f * fbytes.
 int launch_decompress(myyuv_hip_ctx* c, const FrameGeom& G, const void* d_in,
-                      const uint32_t* d_size, uint32_t cap, void* d_out, hipStream_t s) {
+                      const uint32_t* d_size, uint32_t cap, void* d_out, hipStream_t s,
+                      unsigned long long* err = nullptr) {
   const uint32_t nf = G.nframes;
   const uint32_t nblk = G.cum[3];
   const uint32_t ntiles = ceil_div(nblk, kScanTile);
   const QTables* qt = c->qtd.as<const QTables>();
-  unsigned long long* err = c->err.as<unsigned long long>();
+  if (!err) err = c->err.as<unsigned long long>();
   StreamDesc* desc = c->desc.as<StreamDesc>();
   const uint8_t* in = static_cast<const uint8_t*>(d_in);
   int e = 0;
@@ -715,8 +723,20 @@ void myyuv_hip_destroy(myyuv_hip_handle c) {
   (void)hipEventDestroy(c->done);
   DevBuf* bufs[] = {&c->frame, &c->coef, &c->stage, &c->oslots, &c->tinfo, &c->srcoff, &c->sizes, &c->loff, &c->tiles, &c->payload,
                     &c->err,   &c->qtd,  &c->psize, &c->desc,  &c->work,  &c->status, &c->sink,
-                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes, &c->fix, &c->binfo};
+                    &c->bmp,   &c->rmask, &c->zq, &c->bsizes, &c->fix, &c->binfo,
+                    &c->pin[0], &c->pin[1], &c->pout[0], &c->pout[1], &c->psz[0], &c->psz[1],
+                    &c->perr[0], &c->perr[1]};
   for (auto* b : bufs) b->release();
+  if (c->cin) {
+    (void)hipStreamSynchronize(c->cin);
+    (void)hipStreamSynchronize(c->cout);
+    (void)hipStreamDestroy(c->cin);
+    (void)hipStreamDestroy(c->cout);
+    for (auto& row : c->pev)
+      for (auto e : row) (void)hipEventDestroy(e);
+    (void)hipHostFree(c->hsz);
+    (void)hipHostFree(c->herr);
+  }
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -913,46 +933,6 @@ int myyuv_gpu_dct_compress(myyuv_hip_handle c, const uint8_t* iyuv, uint32_t w, 
   return 0;
 }
 
-int myyuv_gpu_dct_compress_batch(myyuv_hip_handle c, const uint8_t* iyuv, uint32_t nframes, uint32_t w,
-                                 uint32_t h, const uint8_t q[3], uint8_t* payloads, uint32_t cap,
-                                 uint32_t* sizes) {
-  if (!c || !iyuv || !payloads || !sizes || !q || nframes == 0) return MYYUV_E_ARG;
-  for (int p = 0; p < 3; p++)
-    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
-  FrameGeom G;
-  int e = make_geom(w, h, G);
-  if (e || (e = set_batch(G, nframes))) return e;
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  hipStream_t s = c->stream;
-  StreamOrder so(c, s);
-  const size_t fbytes = (size_t)w * h * 3 / 2;
-  const uint32_t dcap = (myyuv_dct_payload_bound(w, h) + 3) & ~3u;  // device slot per frame
-  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
-  if (c->frame.grow(fbytes * nframes) || c->payload.grow((size_t)dcap * nframes) ||
-      c->bsizes.grow((size_t)4 * nframes))
-    return MYYUV_E_HIP;
-  if (reset_err(c, s)) return MYYUV_E_HIP;
-  if (h2d(c, c->frame.p, iyuv, fbytes * nframes, s)) return MYYUV_E_HIP;
-  if ((e = launch_compress(c, G, c->frame.p, c->payload.p, dcap, c->bsizes.as<uint32_t>(), s))) return e;
-  if (hipMemcpyAsync(sizes, c->bsizes.p, (size_t)4 * nframes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return MYYUV_E_HIP;
-  int64_t bad = -1;
-  if ((e = read_err(c, s, &bad))) {
-    (void)reset_err(c, s);
-    return e;
-  }
-  for (uint32_t f = 0; f < nframes; f++)
-    if (sizes[f] > cap) return MYYUV_E_CAPACITY;
-  for (uint32_t f = 0; f < nframes; f++)
-    if (d2h(c, payloads + (size_t)f * cap, static_cast<uint8_t*>(c->payload.p) + (size_t)f * dcap, sizes[f], s))
-      return MYYUV_E_HIP;
-  if (hipStreamSynchronize(s) != hipSuccess) return MYYUV_E_HIP;
-  if (c->prof) drain_profile(c);
-  return 0;
-}
-
 int myyuv_gpu_dct_decompress(myyuv_hip_handle c, const uint8_t* payload, uint32_t size, uint32_t w,
                              uint32_t h, const uint8_t q[3], uint8_t* iyuv, int64_t* bad_block) {
   if (bad_block) *bad_block = -1;
@@ -990,6 +970,272 @@ int myyuv_gpu_dct_decompress(myyuv_hip_handle c, const uint8_t* payload, uint32_
   if (d2h(c, iyuv, c->frame.p, fbytes, s)) return MYYUV_E_HIP;
   if (c->prof) drain_profile(c);
   return 0;
+}
+
+// ---- host-buffer batches, pipelined ------------------
+//
+// The batch is cut into chunks of B frames, alternating between two device
+// slots.  Chunk k's host -> device copies run on cin while chunk k-1's kernels
+// run on the context's stream and chunk k-2's results go back on cout, so the
+// PCIe transfers of both directions and the kernels overlap; the host waits
+// only for a chunk's sizes and error word (pinned, copied behind its
+// kernels) before it queues that chunk's device -> host copies.  Each copy
+// goes straight between the caller's (pageable) buffers and the slot.
+namespace {
+
+constexpr uint32_t kPipeMaxChunk = 8;
+constexpr size_t kPipeSlotBytes = (size_t)2 << 30;  // per slot: chunk frames x (input + output) bytes
+
+// frames per chunk: about 8 chunks per batch (the first chunk's upload and
+// the last one's download are not overlapped), at most kPipeMaxChunk and
+// within the slot budget
+uint32_t pipe_chunk(uint32_t nf, size_t per_frame) {
+  uint32_t b = std::max(1u, std::min(kPipeMaxChunk, nf / 8));
+  while (b > 1 && (size_t)b * per_frame > kPipeSlotBytes) b--;
+  return b;
+}
+
+int pipe_init(myyuv_hip_ctx* c) {
+  if (c->cin) return 0;
+  if (hipStreamCreateWithFlags(&c->cin, hipStreamNonBlocking) != hipSuccess) return MYYUV_E_HIP;
+  if (hipStreamCreateWithFlags(&c->cout, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipStreamDestroy(c->cin);
+    c->cin = nullptr;
+    return MYYUV_E_HIP;
+  }
+  int e = 0;
+  for (auto& row : c->pev)
+    for (auto& ev : row) e |= hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess;
+  e |= hipHostMalloc((void**)&c->hsz, 2 * kPipeMaxChunk * 4, hipHostMallocDefault) != hipSuccess;
+  e |= hipHostMalloc((void**)&c->herr, 2 * 8, hipHostMallocDefault) != hipSuccess;
+  for (int k = 0; k < 2; k++) {
+    e |= c->psz[k].grow(kPipeMaxChunk * 4);
+    e |= c->perr[k].grow(8);
+    if (!e) e |= hipMemset(c->perr[k].p, 0xFF, 8) != hipSuccess;
+  }
+  return e ? MYYUV_E_HIP : 0;
+}
+
+// Waits for every pipeline stream (an early return must not leave copies to
+// or from the caller's buffers in flight).
+struct PipeDrain {
+  myyuv_hip_ctx* c;
+  ~PipeDrain() {
+    (void)hipStreamSynchronize(c->cin);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->cout);
+  }
+};
+
+// A chunk's error word (read_err's encoding) -> code, with the failing block
+// made batch-global (chunk's first frame f0, nblk blocks per frame).
+int chunk_err(unsigned long long v, uint32_t f0, uint32_t nblk, int64_t* bad_block) {
+  if (v == ~0ull) return 0;
+  const uint64_t key = v >> 8;
+  if (bad_block) *bad_block = key == 0 ? -1 : (int64_t)(key >> 1) + (int64_t)f0 * nblk;
+  return (int)(v & 0xFF);
+}
+
+int compress_frames(myyuv_hip_ctx* c, const uint8_t* const* frames, uint32_t nf, uint32_t w, uint32_t h,
+                    const uint8_t q[3], myyuv_payload_alloc_fn alloc, void* user, uint32_t* sizes) {
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e) return e;
+  const size_t fb = (size_t)w * h * 3 / 2;
+  const uint32_t dcap = (myyuv_dct_payload_bound(w, h) + 3) & ~3u;  // device slot per frame
+  const uint32_t B = pipe_chunk(nf, fb + dcap);
+  FrameGeom GB = G;
+  if ((e = set_batch(GB, B))) return e;
+  hipStream_t s = c->stream;
+  StreamOrder so(c, s);
+  if ((e = pipe_init(c)) || (e = reserve(c, GB)) || (e = set_qtables(c, q, s))) return e;
+  for (int k = 0; k < 2; k++)
+    if (c->pin[k].grow(fb * B) || c->pout[k].grow((size_t)dcap * B)) return MYYUV_E_HIP;
+  PipeDrain drain{c};
+  const uint32_t nchunks = ceil_div(nf, B);
+  // chunk k's sizes and error word are on the host: its payloads go back
+  auto finish = [&](uint32_t k) -> int {
+    const uint32_t sl = k & 1, f0 = k * B, n = std::min(B, nf - f0);
+    if (hipEventSynchronize(c->pev[1][sl]) != hipSuccess) return MYYUV_E_HIP;
+    if (int ce = chunk_err(c->herr[sl], f0, G.cum[3], nullptr)) return ce;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t size = c->hsz[sl * kPipeMaxChunk + i];
+      sizes[f0 + i] = size;
+      uint8_t* dst = alloc(user, f0 + i, size);
+      if (!dst) return MYYUV_E_CAPACITY;
+      if (hipMemcpyAsync(dst, c->pout[sl].as<uint8_t>() + (size_t)i * dcap, size, hipMemcpyDeviceToHost,
+                         c->cout) != hipSuccess)
+        return MYYUV_E_HIP;
+    }
+    return hipEventRecord(c->pev[2][sl], c->cout) == hipSuccess ? 0 : MYYUV_E_HIP;
+  };
+  for (uint32_t k = 0; k < nchunks; k++) {
+    const uint32_t sl = k & 1, f0 = k * B, n = std::min(B, nf - f0);
+    FrameGeom GK = G;
+    if ((e = set_batch(GK, n))) return e;
+    // upload (slot free once chunk k-2's kernels have read it)
+    if (k >= 2 && hipStreamWaitEvent(c->cin, c->pev[1][sl], 0) != hipSuccess) return MYYUV_E_HIP;
+    for (uint32_t i = 0; i < n; i++)
+      if (hipMemcpyAsync(c->pin[sl].as<uint8_t>() + i * fb, frames[f0 + i], fb, hipMemcpyHostToDevice, c->cin) !=
+          hipSuccess)
+        return MYYUV_E_HIP;
+    if (hipEventRecord(c->pev[0][sl], c->cin) != hipSuccess) return MYYUV_E_HIP;
+    // kernels (output slot free once chunk k-2's payloads are back)
+    if (hipStreamWaitEvent(s, c->pev[0][sl], 0) != hipSuccess ||
+        (k >= 2 && hipStreamWaitEvent(s, c->pev[2][sl], 0) != hipSuccess))
+      return MYYUV_E_HIP;
+    unsigned long long* perr = c->perr[sl].as<unsigned long long>();
+    if ((e = launch_compress(c, GK, c->pin[sl].p, c->pout[sl].p, dcap, c->psz[sl].as<uint32_t>(), s, perr)))
+      return e;
+    if (hipMemcpyAsync(c->hsz + sl * kPipeMaxChunk, c->psz[sl].p, (size_t)n * 4, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipMemcpyAsync(c->herr + sl, perr, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemsetAsync(perr, 0xFF, 8, s) != hipSuccess || hipEventRecord(c->pev[1][sl], s) != hipSuccess)
+      return MYYUV_E_HIP;
+    if (k >= 1 && (e = finish(k - 1))) return e;
+  }
+  if ((e = finish(nchunks - 1))) return e;
+  if (hipStreamSynchronize(c->cout) != hipSuccess) return MYYUV_E_HIP;
+  if (c->prof) drain_profile(c);
+  return 0;
+}
+
+int decompress_frames(myyuv_hip_ctx* c, const uint8_t* const* payloads, const uint32_t* psizes, uint32_t nf,
+                      uint32_t w, uint32_t h, const uint8_t q[3], uint8_t* const* frames, int64_t* bad_block) {
+  FrameGeom G;
+  int e = make_geom(w, h, G);
+  if (e) return e;
+  const size_t fb = (size_t)w * h * 3 / 2;
+  uint32_t icap = 4;  // device slot per stream: the longest, 4-aligned
+  for (uint32_t f = 0; f < nf; f++) icap = std::max(icap, (psizes[f] + 3u) & ~3u);
+  const uint32_t B = pipe_chunk(nf, fb + icap);
+  FrameGeom GB = G;
+  if ((e = set_batch(GB, B))) return e;
+  hipStream_t s = c->stream;
+  StreamOrder so(c, s);
+  if ((e = pipe_init(c)) || (e = reserve(c, GB)) || (e = set_qtables(c, q, s))) return e;
+  for (int k = 0; k < 2; k++)
+    if (c->pin[k].grow((size_t)icap * B) || c->pout[k].grow(fb * B)) return MYYUV_E_HIP;
+  PipeDrain drain{c};
+  const uint32_t nchunks = ceil_div(nf, B);
+  auto finish = [&](uint32_t k) -> int {
+    const uint32_t sl = k & 1, f0 = k * B, n = std::min(B, nf - f0);
+    if (hipEventSynchronize(c->pev[1][sl]) != hipSuccess) return MYYUV_E_HIP;
+    if (int ce = chunk_err(c->herr[sl], f0, G.cum[3], bad_block)) return ce;
+    for (uint32_t i = 0; i < n; i++)
+      if (hipMemcpyAsync(frames[f0 + i], c->pout[sl].as<uint8_t>() + i * fb, fb, hipMemcpyDeviceToHost, c->cout) !=
+          hipSuccess)
+        return MYYUV_E_HIP;
+    return hipEventRecord(c->pev[2][sl], c->cout) == hipSuccess ? 0 : MYYUV_E_HIP;
+  };
+  for (uint32_t k = 0; k < nchunks; k++) {
+    const uint32_t sl = k & 1, f0 = k * B, n = std::min(B, nf - f0);
+    FrameGeom GK = G;
+    if ((e = set_batch(GK, n))) return e;
+    if (k >= 2 && hipStreamWaitEvent(c->cin, c->pev[1][sl], 0) != hipSuccess) return MYYUV_E_HIP;
+    uint8_t* slot = c->pin[sl].as<uint8_t>();
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t sz = psizes[f0 + i], cap_i = (sz + 3u) & ~3u;
+      // the stream's last word zero-padded (the scan reads whole words), then the bytes
+      if ((cap_i >= 4 && hipMemsetAsync(slot + (size_t)i * icap + cap_i - 4, 0, 4, c->cin) != hipSuccess) ||
+          hipMemcpyAsync(slot + (size_t)i * icap, payloads[f0 + i], sz, hipMemcpyHostToDevice, c->cin) != hipSuccess)
+        return MYYUV_E_HIP;
+    }
+    if (hipMemcpyAsync(c->psz[sl].p, psizes + f0, (size_t)n * 4, hipMemcpyHostToDevice, c->cin) != hipSuccess ||
+        hipEventRecord(c->pev[0][sl], c->cin) != hipSuccess)
+      return MYYUV_E_HIP;
+    if (hipStreamWaitEvent(s, c->pev[0][sl], 0) != hipSuccess ||
+        (k >= 2 && hipStreamWaitEvent(s, c->pev[2][sl], 0) != hipSuccess))
+      return MYYUV_E_HIP;
+    unsigned long long* perr = c->perr[sl].as<unsigned long long>();
+    if ((e = launch_decompress(c, GK, slot, c->psz[sl].as<const uint32_t>(), icap, c->pout[sl].p, s, perr)))
+      return e;
+    if (hipMemcpyAsync(c->herr + sl, perr, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemsetAsync(perr, 0xFF, 8, s) != hipSuccess || hipEventRecord(c->pev[1][sl], s) != hipSuccess)
+      return MYYUV_E_HIP;
+    if (k >= 1 && (e = finish(k - 1))) return e;
+  }
+  if ((e = finish(nchunks - 1))) return e;
+  if (hipStreamSynchronize(c->cout) != hipSuccess) return MYYUV_E_HIP;
+  if (c->prof) drain_profile(c);
+  return 0;
+}
+
+struct SlotAlloc {
+  uint8_t* base;
+  uint32_t cap;
+};
+uint8_t* slot_alloc(void* user, uint32_t frame, uint32_t size) {
+  const SlotAlloc* a = static_cast<const SlotAlloc*>(user);
+  return size <= a->cap ? a->base + (size_t)frame * a->cap : nullptr;
+}
+
+int check_q(const uint8_t q[3]) {
+  for (int p = 0; p < 3; p++)
+    if (q[p] < 1 || q[p] > 100) return MYYUV_E_QUALITY;
+  return 0;
+}
+
+}  // namespace
+
+int myyuv_gpu_dct_compress_frames(myyuv_hip_handle c, const uint8_t* const* frames, uint32_t nframes, uint32_t w,
+                                  uint32_t h, const uint8_t q[3], myyuv_payload_alloc_fn alloc, void* user,
+                                  uint32_t* sizes) {
+  if (!c || !frames || !alloc || !sizes || !q || nframes == 0) return MYYUV_E_ARG;
+  for (uint32_t f = 0; f < nframes; f++)
+    if (!frames[f]) return MYYUV_E_ARG;
+  if (int e = check_q(q)) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return compress_frames(c, frames, nframes, w, h, q, alloc, user, sizes);
+}
+
+int myyuv_gpu_dct_compress_batch(myyuv_hip_handle c, const uint8_t* iyuv, uint32_t nframes, uint32_t w,
+                                 uint32_t h, const uint8_t q[3], uint8_t* payloads, uint32_t cap,
+                                 uint32_t* sizes) {
+  if (!c || !iyuv || !payloads || !sizes || !q || nframes == 0) return MYYUV_E_ARG;
+  if (int e = check_q(q)) return e;
+  const size_t fb = (size_t)w * h * 3 / 2;
+  std::vector<const uint8_t*> fr(nframes);
+  for (uint32_t f = 0; f < nframes; f++) fr[f] = iyuv + f * fb;
+  SlotAlloc a{payloads, cap};
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return compress_frames(c, fr.data(), nframes, w, h, q, slot_alloc, &a, sizes);
+}
+
+int myyuv_gpu_dct_decompress_frames(myyuv_hip_handle c, const uint8_t* const* payloads, const uint32_t* sizes,
+                                    uint32_t nframes, uint32_t w, uint32_t h, const uint8_t q[3],
+                                    uint8_t* const* frames, int64_t* bad_block) {
+  if (bad_block) *bad_block = -1;
+  if (!c || !payloads || !sizes || !frames || !q || nframes == 0) return MYYUV_E_ARG;
+  for (uint32_t f = 0; f < nframes; f++)
+    if (!payloads[f] || !frames[f]) return MYYUV_E_ARG;
+  if (int e = check_q(q)) return e;
+  // every stream's DCTYUV::load checks first (DCT.cpp:454; the single-frame
+  // call's order), frame by frame
+  for (uint32_t f = 0; f < nframes; f++)
+    if (int e = host_parse_headers(payloads[f], sizes[f])) return e;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return decompress_frames(c, payloads, sizes, nframes, w, h, q, frames, bad_block);
+}
+
+int myyuv_gpu_dct_decompress_batch(myyuv_hip_handle c, const uint8_t* payloads, const uint32_t* sizes, uint32_t cap,
+                                   uint32_t nframes, uint32_t w, uint32_t h, const uint8_t q[3], uint8_t* iyuv,
+                                   int64_t* bad_block) {
+  if (bad_block) *bad_block = -1;
+  if (!c || !payloads || !sizes || !iyuv || !q || nframes == 0) return MYYUV_E_ARG;
+  for (uint32_t f = 0; f < nframes; f++)
+    if (sizes[f] > cap) return MYYUV_E_ARG;
+  const size_t fb = (size_t)w * h * 3 / 2;
+  std::vector<const uint8_t*> in(nframes);
+  std::vector<uint8_t*> out(nframes);
+  for (uint32_t f = 0; f < nframes; f++) {
+    in[f] = payloads + (size_t)f * cap;
+    out[f] = iyuv + f * fb;
+  }
+  return myyuv_gpu_dct_decompress_frames(c, in.data(), sizes, nframes, w, h, q, out.data(), bad_block);
 }
 
 int myyuv_hip_profile(myyuv_hip_handle c, int enable) {

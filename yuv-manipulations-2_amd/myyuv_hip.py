@@ -34,10 +34,13 @@ EXPORTS = [
     "myyuv_hip_profile", "myyuv_hip_profile_kernels", "myyuv_hip_kernel_stats", "myyuv_gpu_fdct_blocks",
     "myyuv_gpu_huff_encode_blocks", "myyuv_hip_reserve_batch", "myyuv_gpu_dct_compress_batch_device",
     "myyuv_gpu_dct_decompress_batch_device", "myyuv_gpu_bmp_to_iyuv", "myyuv_gpu_bmp_to_iyuv_device",
-    "myyuv_gpu_dct_compress_batch",
+    "myyuv_gpu_dct_compress_batch", "myyuv_gpu_dct_compress_frames", "myyuv_gpu_dct_decompress_frames",
+    "myyuv_gpu_dct_decompress_batch",
 ]
 
 _lib = None
+# myyuv_payload_alloc_fn
+PAYLOAD_ALLOC = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32)
 
 
 class CodecError(RuntimeError):
@@ -103,6 +106,12 @@ def load():
     L.myyuv_gpu_bmp_to_iyuv.argtypes = [vp, u8p, i32, i32, ctypes.c_uint16, u8p]
     L.myyuv_gpu_bmp_to_iyuv_device.argtypes = [vp, vp, i32, i32, ctypes.c_uint16, vp, vp]
     L.myyuv_gpu_dct_compress_batch.argtypes = [vp, u8p, u32, u32, u32, u8p, u8p, u32, ctypes.POINTER(u32)]
+    L.myyuv_gpu_dct_decompress_batch.argtypes = [vp, u8p, ctypes.POINTER(u32), u32, u32, u32, u32, u8p, u8p,
+                                                 ctypes.POINTER(ctypes.c_int64)]
+    L.myyuv_gpu_dct_decompress_frames.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u32), u32, u32, u32, u8p,
+                                                  ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64)]
+    L.myyuv_gpu_dct_compress_frames.argtypes = [vp, ctypes.POINTER(vp), u32, u32, u32, u8p, PAYLOAD_ALLOC, vp,
+                                                ctypes.POINTER(u32)]
     L.myyuv_debug_tinfo_guard.argtypes = [vp, u32, ctypes.c_int, ctypes.POINTER(u32)]  # diagnostic
     _lib = L
     return L
@@ -238,6 +247,63 @@ class Codec:
         if rc:
             raise CodecError(rc)
         return [out[i * cap: i * cap + sizes[i]].tobytes() for i in range(n)]
+
+    def compress_frames(self, frames, w, h, q):
+        """Host-buffer batch through the pointer-array entry point: each
+        payload is written into a buffer sized once its length is known."""
+        n = len(frames)
+        fb = w * h * 3 // 2
+        srcs = [np.frombuffer(bytes(f), np.uint8) for f in frames]
+        for i, a in enumerate(srcs):
+            if a.size != fb:
+                raise ValueError(f"frame {i}: {a.size} bytes, a {w}x{h} IYUV frame has {fb}")
+        ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in srcs])
+        outs = [None] * n
+
+        def alloc(_user, f, size):
+            outs[f] = np.empty(max(size, 1), np.uint8)
+            return outs[f].ctypes.data
+
+        cb = PAYLOAD_ALLOC(alloc)
+        sizes = (ctypes.c_uint32 * n)()
+        rc = load().myyuv_gpu_dct_compress_frames(self._h, ptrs, n, w, h, _u8(_q(q)), cb, None, sizes)
+        if rc:
+            raise CodecError(rc)
+        return [outs[i][: sizes[i]].tobytes() for i in range(n)]
+
+    def decompress_batch(self, payloads, w, h, q):
+        """Host-buffer batch decompress (pipelined): a list of DCTYUV
+        payloads of one geometry and quality -> their IYUV frames."""
+        n = len(payloads)
+        fb = w * h * 3 // 2
+        cap = max(len(p) for p in payloads)
+        src = np.zeros(n * cap, np.uint8)
+        sizes = (ctypes.c_uint32 * n)()
+        for i, p in enumerate(payloads):
+            src[i * cap: i * cap + len(p)] = np.frombuffer(bytes(p), np.uint8)
+            sizes[i] = len(p)
+        out = np.empty(n * fb, np.uint8)
+        bad = ctypes.c_int64(-1)
+        rc = load().myyuv_gpu_dct_decompress_batch(self._h, _u8(src), sizes, cap, n, w, h, _u8(_q(q)), _u8(out),
+                                                   ctypes.byref(bad))
+        if rc:
+            raise CodecError(rc, bad.value)
+        return [out[i * fb:(i + 1) * fb].tobytes() for i in range(n)]
+
+    def decompress_frames(self, payloads, w, h, q):
+        """The pointer-array form of decompress_batch."""
+        n = len(payloads)
+        fb = w * h * 3 // 2
+        srcs = [np.frombuffer(bytes(p), np.uint8) for p in payloads]
+        outs = [np.empty(fb, np.uint8) for _ in range(n)]
+        ip = (ctypes.c_void_p * n)(*[a.ctypes.data for a in srcs])
+        op = (ctypes.c_void_p * n)(*[a.ctypes.data for a in outs])
+        sizes = (ctypes.c_uint32 * n)(*[a.size for a in srcs])
+        bad = ctypes.c_int64(-1)
+        rc = load().myyuv_gpu_dct_decompress_frames(self._h, ip, sizes, n, w, h, _u8(_q(q)), op, ctypes.byref(bad))
+        if rc:
+            raise CodecError(rc, bad.value)
+        return [o.tobytes() for o in outs]
 
     def bmp_to_iyuv(self, bmp_data, width, height, bit_count):
         """BMP::data (as stored; signed header width/height) -> IYUV bytes,
