@@ -910,8 +910,9 @@ def host_batch_rate(codec_mod, raw, w, h, q, nframes, reps):
         if any(int(sizes[f]) != n0 for f in range(nframes)) or \
                 any(sha(pay[f * cap: f * cap + n0].tobytes()) != sha(pay[:n0].tobytes()) for f in (1, nframes - 1)):
             raise SystemExit("host batch: frames of one input differ")
-        if out[:fb].tobytes() != raw or out[(nframes - 1) * fb:].tobytes() != raw:
-            raise SystemExit("host batch: decoded frames differ from the input decode")
+        dec1 = c.decompress(pay[:n0].tobytes(), w, h, (q, q, q))  # the single-frame call
+        if out[:fb].tobytes() != dec1 or out[(nframes - 1) * fb:].tobytes() != dec1:
+            raise SystemExit("host batch: decoded frames differ from the single-frame decode")
         mc, md = statistics.median(tc), statistics.median(td)
         mp = w * h / 1e6 * nframes
         pcie = nframes * 2 * (fb + n0)

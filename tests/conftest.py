@@ -33,27 +33,45 @@ def oracle():
     return O
 
 
-@pytest.fixture(scope="session", params=["split", "fused"])
-def codec(request):
-    """A codec context per kernel arrangement: "split" (K1 -> K2 and K5 -> K6
-    through HBM) and "fused" (the single-pass encoder k_encode_tile and the
-    single-pass decoder k_decode_idct, the decoder's default; MYYUV_ENCODER /
-    MYYUV_DECODER are read when the context is created).  Every test taking
-    `codec` runs on both."""
+def _codec_with(env):
     import myyuv_hip
 
-    vals = {"MYYUV_ENCODER": request.param, "MYYUV_DECODER": request.param}
-    old = {k: os.environ.get(k) for k in vals}
-    for k, v in vals.items():
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
         os.environ[k] = v
     try:
-        c = myyuv_hip.Codec(0)
+        return myyuv_hip.Codec(0)
     finally:
-        for k in vals:
+        for k in env:
             if old[k] is None:
                 del os.environ[k]
             else:
                 os.environ[k] = old[k]
+
+
+# kernel arrangements (MYYUV_ENCODER / MYYUV_DECODER are read when a context
+# is created): "default" is the product (K1 -> K2 through HBM, the fused
+# decoder k_decode_idct), "split" K1 -> K2 and K5 -> K6 through HBM
+ARRANGEMENTS = {"default": {"MYYUV_ENCODER": "split", "MYYUV_DECODER": "fused"},
+                "split": {"MYYUV_ENCODER": "split", "MYYUV_DECODER": "split"}}
+
+
+@pytest.fixture(scope="session", params=list(ARRANGEMENTS))
+def codec(request):
+    """A codec context per kernel arrangement (ARRANGEMENTS); every test
+    taking `codec` runs on both."""
+    c = _codec_with(ARRANGEMENTS[request.param])
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="session")
+def fused_encoder():
+    """A context with the fused single-pass encoder k_encode_tile
+    (MYYUV_ENCODER=fused).  It measured slower than K1 -> K2
+    in every round, so it is not the product and not in the
+    `codec` matrix; tests/test_gpu_fused_encoder.py keeps it bit-exact."""
+    c = _codec_with({"MYYUV_ENCODER": "fused", "MYYUV_DECODER": "fused"})
     yield c
     c.close()
 

@@ -43,12 +43,17 @@ def test_host_batch_roundtrip_matches_oracle(codec, oracle, golden, n):
 
 
 def test_host_batch_big_frames(codec, chef_big):
-    """Three 4032x3008 frames: the pinned q50 stream each, and back to the
-    pinned decode."""
+    """Three 4032x3008 frames: the golden DCT-50 stream decodes to the pinned
+    frame, which compresses to the pinned q50 stream, which decodes as the
+    single-frame call does (hashes: a byte diff of 18 MB is slow)."""
     f, raw = chef_big
-    pays = codec.compress_frames([raw] * 3, f.width, f.height, (50, 50, 50))
-    assert [hashlib.sha256(p).hexdigest() for p in pays] == [BIG_Q50_SHA] * 3
-    assert codec.decompress_batch(pays, f.width, f.height, (50, 50, 50)) == [raw] * 3
+    w, h, q = f.width, f.height, (50, 50, 50)
+    sha = lambda b: hashlib.sha256(b).hexdigest()  # noqa: E731
+    assert [sha(o) for o in codec.decompress_batch([f.data] * 3, w, h, q)] == [sha(raw)] * 3
+    pays = codec.compress_frames([raw] * 3, w, h, q)
+    assert [sha(p) for p in pays] == [BIG_Q50_SHA] * 3
+    want = sha(codec.decompress(pays[0], w, h, q))
+    assert [sha(o) for o in codec.decompress_frames(pays, w, h, q)] == [want] * 3
 
 
 def test_host_batch_decode_error_names_the_block(codec, oracle, golden):

@@ -26,16 +26,21 @@ constexpr uint32_t kSinkQuads = 192, kSinkSlots = MYYUV_SINK_SLOTS;
 #define MYYUV_FIX_WAVES 4
 #endif
 constexpr uint32_t kFixWaves = MYYUV_FIX_WAVES;
-// K1 -> k_fdct_fix: the unproven units in kFixLists lists (unit ua in list
-// ua % kFixLists), so their appends spread over as many atomic counters: the
-// counters of parity p (launches alternate) one per 128-B line from word 0,
-// list c from word kFixHeader at c * ceil(units / kFixLists)
+// K1 -> k_fdct_fix: the unproven BLOCKS (entry ua * 16 + b: block slot b of
+// unit ua) in kFixLists lists (unit ua's blocks in list ua % kFixLists), so
+// the appends spread over as many atomic counters: the counters of parity p
+// (launches alternate) one per 128-B line from word 0, list c from word
+// kFixHeader at c * fix_list_cap(units) (16 blocks per unit: no list can
+// overflow)
 constexpr uint32_t kFixLists = 32, kFixHeader = 2 * kFixLists * 32;
 __host__ __device__ __forceinline__ uint32_t* fix_count(uint32_t* fix, uint32_t par, uint32_t c) {
   return fix + (par * kFixLists + c) * 32u;
 }
+__host__ __device__ __forceinline__ uint32_t fix_list_cap(uint32_t units) {
+  return 16u * ((units + kFixLists - 1) / kFixLists);
+}
 __host__ __device__ __forceinline__ size_t fix_words(uint32_t units) {
-  return kFixHeader + (size_t)kFixLists * ((units + kFixLists - 1) / kFixLists);
+  return kFixHeader + (size_t)kFixLists * fix_list_cap(units);
 }
 constexpr int kMaxChunk = 160;
 
@@ -271,10 +276,9 @@ __host__ __device__ __forceinline__ uint32_t tile_of_block(const FrameGeom& G, u
   return f * G.tcum[3] + G.tcum[p] + (l - G.cum[p]) / kK2Group;
 }
 
-// list c of K1's unproven units (see fix_count)
+// list c of K1's unproven blocks (see fix_count)
 __host__ __device__ __forceinline__ uint32_t* fix_list(uint32_t* fix, const FrameGeom& G, uint32_t c) {
-  const uint32_t units = G.ucum[3] * G.nframes;
-  return fix + kFixHeader + (size_t)c * ((units + kFixLists - 1) / kFixLists);
+  return fix + kFixHeader + (size_t)c * fix_list_cap(G.ucum[3] * G.nframes);
 }
 
 }  // namespace myyuv_gpu

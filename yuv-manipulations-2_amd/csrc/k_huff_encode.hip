@@ -1395,7 +1395,7 @@ __global__ __launch_bounds__(kK2Group, 3) void k_encode_tile(const uint8_t* __re
     *reinterpret_cast<uint2*>(img + 16u * q) = make_uint2(rows.px[i].x, rows.px[i].y);
     *reinterpret_cast<uint2*>(img + 16u * q + 8u) = make_uint2(rows.px[i].z, rows.px[i].w);
     wave_sync();
-    fdct_core(img, tb, q, s_q, p, [&](const uint32_t (&c)[16]) {
+    fdct_core(img, tb, q, s_q, p, [&](const uint32_t (&c)[16], bool) {
       uint4 lo, hi;
       uint32_t rm;
       pack_quads(c, q, lo, hi, rm);

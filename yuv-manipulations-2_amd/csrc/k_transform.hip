@@ -208,33 +208,43 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
     nx = load_rows(frame, G, ua + stride < nall ? ua + stride : ua, b, q);
     wave_sync();
 
-    // stores of lanes past the plane's end go to the sink (no branch: see
-    // load_rows)
-    uint4* dlo = live ? coef + coef_quad(g, 2 * q) : sink + lane;
-    uint4* dhi = live ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
-
-    auto store = [&](const uint32_t (&c)[16]) {
-      store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
+    // stores of lanes past the plane's end, and of blocks left to the exact
+    // path, go to the sink (no branch: see load_rows)
+    auto store = [&](const uint32_t (&c)[16], bool keep) {
+      const bool lv = live && keep;
+      uint4* dlo = lv ? coef + coef_quad(g, 2 * q) : sink + lane;
+      uint4* dhi = lv ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
+      store_block_rows(c, q, lane, lv, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
     };
     uint32_t xr[4];
     fdct_load(img, q, xr);
-    if (!fdct_fast(xr, tb, q, sqr, U.p, store) && lane == 0) {
+    const uint64_t bad = fdct_fast<true>(xr, tb, q, sqr, U.p, store);
+    if (bad != 0) {  // (wave-uniform) the unproven blocks, listed by their lane 4b
+      const bool mine = ((bad >> lane) & 1u) && q == 0 && live;
+      const uint64_t m = __ballot(mine);
       const uint32_t c = ua % kFixLists;
-      // (a launch lists each unit at most once, so a count below the list's
+      uint32_t base = 0;
+      // (a launch lists each block at most once, so a count below the list's
       // capacity is guaranteed while k_fdct_fix resets the counts; the clamp
       // keeps a stale count, e.g. a diagnostic skip of the fix kernel, in bounds)
-      const uint32_t idx = atomicAdd(fix_count(fix, par, c), 1u);
-      if (idx < (nall + kFixLists - 1) / kFixLists) fix_list(fix, G, c)[idx] = ua;
+      if (lane == 0 && m != 0) base = atomicAdd(fix_count(fix, par, c), (uint32_t)__popcll(m));
+      base = __builtin_amdgcn_readfirstlane(base);
+      const uint32_t idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (mine && idx < fix_list_cap(nall)) fix_list(fix, G, c)[idx] = ua * kXfUnit + b;
     }
   }
 }
 
-// K1's exact path for the units K1 listed (kFixLists lists, the counts of
-// parity par): a wave per listed unit, the reference's order (fdct_exact),
-// the same stores.  Wave w takes list w % kFixLists (the grid's waves are a
-// multiple of kFixLists).  Workgroup 0 zeroes the other parity's counts, which
-// the next K1 fills (the previous fix launch, their reader, is done: stream
-// order).
+// K1's exact path for the blocks K1 listed (kFixLists lists, the counts of
+// parity par; entry ua * 16 + b: block slot b of unit ua): a wave takes 16
+// listed blocks at a time, in any planes and frames (lane (b, q) takes
+// entry b: its geometry, plane and Q tables per lane), the reference's order
+// (fdct_exact), the same stores.  Wave w takes list w % kFixLists (the grid's
+// waves are a multiple of kFixLists).  Workgroup 0 zeroes the other parity's
+// counts, which the next K1 fills (the previous fix launch, their reader, is
+// done: stream order).  Per block rather than per unit: at q90 on the bench
+// frame 20 % of the units but 1.8 % of the blocks are unproven
+// (tools/diag/fdct_bfly_check.cpp).
 __global__ __launch_bounds__(64 * kFixWaves) void k_fdct_fix(const uint8_t* __restrict__ frame, FrameGeom G,
                                                   const QTables* __restrict__ qt, uint4* __restrict__ coef,
                                                   uint8_t* __restrict__ rmask, uint32_t* __restrict__ binfo,
@@ -250,7 +260,7 @@ __global__ __launch_bounds__(64 * kFixWaves) void k_fdct_fix(const uint8_t* __re
   const uint32_t gw = blockIdx.x * kFixWaves + (threadIdx.x >> 6), nw = gridDim.x * kFixWaves;
   const uint32_t c = gw % kFixLists;
   const uint32_t n = __builtin_amdgcn_readfirstlane(*fix_count(fix, par, c));
-  if ((threadIdx.x & 63u) == 0 && gw / kFixLists < n) s_any = 1u;
+  if ((threadIdx.x & 63u) == 0 && gw / kFixLists * kXfUnit < n) s_any = 1u;
   __syncthreads();
   if (s_any == 0u) return;  // (uniform over the workgroup)
   stage_zz(szz);
@@ -262,25 +272,26 @@ __global__ __launch_bounds__(64 * kFixWaves) void k_fdct_fix(const uint8_t* __re
   float* tb = tile[threadIdx.x >> 6] + b * kTile;
   uint8_t* img = reinterpret_cast<uint8_t*>(tb);
   const uint32_t* list = fix_list(fix, G, c);
-  for (uint32_t i = gw / kFixLists; i < n; i += nw / kFixLists) {
-    const uint32_t ua = __builtin_amdgcn_readfirstlane(list[i]);
+  for (uint32_t i = gw / kFixLists * kXfUnit; i < n; i += nw / kFixLists * kXfUnit) {
+    // lanes past the list's end redo entry i (a real block) into the sink
+    const bool real = i + b < n;
+    const uint32_t ent = list[real ? i + b : i];
+    const uint32_t ua = ent / kXfUnit, bb = ent % kXfUnit;
     const uint32_t f = div_magic(ua, G.umag);
     const Unit U = unit_of(G, ua - f * G.ucum[3]);
-    const uint32_t local = U.local0 + b;
-    const bool live = local < U.nb;
-    const uint32_t g = f * G.cum[3] + U.cum + local;
-    const uint4 r = load_rows(frame, G, ua, b, q);
-    wave_sync();  // (the previous unit's tile reads are done)
+    const uint32_t g = f * G.cum[3] + U.cum + U.local0 + bb;
+    const uint4 r = load_rows(frame, G, ua, bb, q);
+    wave_sync();  // (the previous blocks' tile reads are done)
     *reinterpret_cast<uint2*>(img + 16u * q) = make_uint2(r.x, r.y);
     *reinterpret_cast<uint2*>(img + 16u * q + 8u) = make_uint2(r.z, r.w);
     wave_sync();
-    uint4* dlo = live ? coef + coef_quad(g, 2 * q) : sink + lane;
-    uint4* dhi = live ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
+    uint4* dlo = real ? coef + coef_quad(g, 2 * q) : sink + lane;
+    uint4* dhi = real ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
     uint32_t xr[4];
     fdct_load(img, q, xr);
     fdct_exact(xr, tb, q, sqr, U.p,
-               [&](const uint32_t (&c)[16]) {
-                 store_block_rows(c, q, lane, live, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
+               [&](const uint32_t (&cc)[16]) {
+                 store_block_rows(cc, q, lane, real, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
                });
   }
 }

@@ -984,6 +984,19 @@ int myyuv_gpu_dct_decompress(myyuv_hip_handle c, const uint8_t* payload, uint32_
 namespace {
 
 constexpr uint32_t kPipeMaxChunk = 8;
+// MYYUV_PIPE_TRACE=1: one stderr line per pipeline step (diagnostic)
+bool pipe_trace() {
+  static int t = -1;
+  if (t < 0) t = std::getenv("MYYUV_PIPE_TRACE") ? 1 : 0;
+  return t == 1;
+}
+#define PIPE_TRACE(...)                   \
+  do {                                    \
+    if (pipe_trace()) {                   \
+      std::fprintf(stderr, __VA_ARGS__);  \
+      std::fflush(stderr);                \
+    }                                     \
+  } while (0)
 constexpr size_t kPipeSlotBytes = (size_t)2 << 30;  // per slot: chunk frames x (input + output) bytes
 
 // frames per chunk: about 8 chunks per batch (the first chunk's upload and
@@ -1056,7 +1069,9 @@ int compress_frames(myyuv_hip_ctx* c, const uint8_t* const* frames, uint32_t nf,
   // chunk k's sizes and error word are on the host: its payloads go back
   auto finish = [&](uint32_t k) -> int {
     const uint32_t sl = k & 1, f0 = k * B, n = std::min(B, nf - f0);
+    PIPE_TRACE("pipe c finish %u: wait kernels\n", k);
     if (hipEventSynchronize(c->pev[1][sl]) != hipSuccess) return MYYUV_E_HIP;
+    PIPE_TRACE("pipe c finish %u: kernels done\n", k);
     if (int ce = chunk_err(c->herr[sl], f0, G.cum[3], nullptr)) return ce;
     for (uint32_t i = 0; i < n; i++) {
       const uint32_t size = c->hsz[sl * kPipeMaxChunk + i];
@@ -1067,12 +1082,15 @@ int compress_frames(myyuv_hip_ctx* c, const uint8_t* const* frames, uint32_t nf,
                          c->cout) != hipSuccess)
         return MYYUV_E_HIP;
     }
+    PIPE_TRACE("pipe c finish %u: downloads queued\n", k);
     return hipEventRecord(c->pev[2][sl], c->cout) == hipSuccess ? 0 : MYYUV_E_HIP;
   };
+  PIPE_TRACE("pipe c: %u frames, chunks of %u\n", nf, B);
   for (uint32_t k = 0; k < nchunks; k++) {
     const uint32_t sl = k & 1, f0 = k * B, n = std::min(B, nf - f0);
     FrameGeom GK = G;
     if ((e = set_batch(GK, n))) return e;
+    PIPE_TRACE("pipe c chunk %u: upload\n", k);
     // upload (slot free once chunk k-2's kernels have read it)
     if (k >= 2 && hipStreamWaitEvent(c->cin, c->pev[1][sl], 0) != hipSuccess) return MYYUV_E_HIP;
     for (uint32_t i = 0; i < n; i++)
@@ -1080,6 +1098,7 @@ int compress_frames(myyuv_hip_ctx* c, const uint8_t* const* frames, uint32_t nf,
           hipSuccess)
         return MYYUV_E_HIP;
     if (hipEventRecord(c->pev[0][sl], c->cin) != hipSuccess) return MYYUV_E_HIP;
+    PIPE_TRACE("pipe c chunk %u: uploads queued\n", k);
     // kernels (output slot free once chunk k-2's payloads are back)
     if (hipStreamWaitEvent(s, c->pev[0][sl], 0) != hipSuccess ||
         (k >= 2 && hipStreamWaitEvent(s, c->pev[2][sl], 0) != hipSuccess))
@@ -1095,7 +1114,9 @@ int compress_frames(myyuv_hip_ctx* c, const uint8_t* const* frames, uint32_t nf,
     if (k >= 1 && (e = finish(k - 1))) return e;
   }
   if ((e = finish(nchunks - 1))) return e;
+  PIPE_TRACE("pipe c: wait downloads\n");
   if (hipStreamSynchronize(c->cout) != hipSuccess) return MYYUV_E_HIP;
+  PIPE_TRACE("pipe c: done\n");
   if (c->prof) drain_profile(c);
   return 0;
 }

@@ -267,9 +267,13 @@ __device__ __forceinline__ void fdct_load(const uint8_t* img, uint32_t q, uint32
 // QTables offsets in the staged LDS copy (sqr): q, r, kb
 constexpr int kSqR = 3 * 64, kSqKb = 2 * 3 * 64, kSqWords = 2 * 3 * 64 + 3 * 8;
 
-template <class Emit>
-__device__ __forceinline__ bool fdct_fast(const uint32_t (&xr)[4], float* tb, uint32_t q, const float* sqr, int p,
-                                          Emit&& emit) {
+// Returns 0 when every output of the unit is proven (all emitted), else the
+// ballot of the lanes whose BLOCK has an unproven output: with kPerBlock the
+// proven blocks are emitted (emit(c, keep): keep false for the others, whose
+// lanes must store nothing), without it nothing is emitted.
+template <bool kPerBlock, class Emit>
+__device__ __forceinline__ uint64_t fdct_fast(const uint32_t (&xr)[4], float* tb, uint32_t q, const float* sqr, int p,
+                                              Emit&& emit) {
   // ---- A = sum |x - 128| over the block (exact: byte SADs against 128, the
   // block's four lanes summed)
   uint32_t a = 0;
@@ -315,9 +319,21 @@ __device__ __forceinline__ bool fdct_fast(const uint32_t (&xr)[4], float* tb, ui
     }
     mx = __builtin_fmaxf(mx, __builtin_fmaf(af, sqr[kSqKb + p * 8 + 2 * q + h], em));
   }
-  if (__builtin_amdgcn_ballot_w64(mx >= 0.5f) != 0) return false;
-  emit(c);  // every output clears the bound: its rounded t is the reference's coefficient
-  return true;
+  const uint64_t bad = __builtin_amdgcn_ballot_w64(mx >= 0.5f);
+  if (bad == 0) {
+    emit(c, true);  // every output clears the bound: its rounded t is the reference's coefficient
+    return 0;
+  }
+  if (!kPerBlock) return bad;
+  // (bad != 0 is wave-uniform: the whole wave runs the quad exchanges) a
+  // block is unproven when any of its four lanes is; the bound is per block
+  // (A and the row factors are the block's own), so the other blocks' outputs
+  // are the reference's
+  uint32_t fb = mx >= 0.5f ? 1u : 0u;
+  fb |= quad_xor1(fb);
+  fb |= quad_xor2(fb);
+  emit(c, fb == 0u);
+  return __builtin_amdgcn_ballot_w64(fb != 0u);
 }
 
 // The unit in the reference's order (the tile tb is rewritten: callers
@@ -361,9 +377,9 @@ __device__ __forceinline__ void fdct_core(const uint8_t* img, float* tb, uint32_
                                           Emit&& emit) {
   uint32_t xr[4];
   fdct_load(img, q, xr);
-  if (__builtin_expect(!fdct_fast(xr, tb, q, sqr, p, emit), 0)) {
+  if (__builtin_expect(fdct_fast<false>(xr, tb, q, sqr, p, emit) != 0, 0)) {
     wave_sync();
-    fdct_exact(xr, tb, q, sqr, p, emit);
+    fdct_exact(xr, tb, q, sqr, p, [&](const uint32_t (&c)[16]) { emit(c, true); });
   }
 }
 
