@@ -57,6 +57,15 @@ constexpr uint32_t kGposQuads = 8 * 64 * 4 / 16;
 #ifndef MYYUV_K5_GROUP
 #define MYYUV_K5_GROUP 2  // positions per "any lane left" test (1 / 2 / 4 / 8: 132.4 / 128.2 / 129.0 / 135.1 us per launch, tools/runs/r3n.sh)
 #endif
+// The symbol loop's arithmetic in full-rate forms (1; 0: as the compiler
+// picks them): the value's stage bit by a 24-bit multiply-add (the code has
+// at most 8 bits; written as a 32-bit product the compiler emits the 64-bit
+// v_mad_u64_u32), and the message's bit count as a register of its own
+// (left packed with the table size, every comparison with it is an SDWA
+// form)
+#ifndef MYYUV_K5_FORMS
+#define MYYUV_K5_FORMS 1
+#endif
 #ifndef MYYUV_K5S_WAVES
 #define MYYUV_K5S_WAVES 5  // the split decoder's K5
 #endif
@@ -184,7 +193,11 @@ __device__ __forceinline__ int parse_table(const Chunk& c, uint32_t s, Table& T,
     gcol[64 * L] = 8 * c.b0 + gb - 11 * F;  // (mod 2^32: the first value's stage bit is 8 b0 + gb)
     F = (F + cL) << 1;
   }
-  T.nbits = nbits;
+  uint32_t nb = nbits;
+#if MYYUV_K5_FORMS
+  asm volatile("" : "+v"(nb));  // (materialised: no WORD_0 selects on h0 in the symbol loop)
+#endif
+  T.nbits = nb;
   T.sbit = 8 * (3 + tb);
   T.tb = tb;
   T.cnt = cnt;
@@ -242,7 +255,12 @@ __device__ __forceinline__ bool decode_regular(const LdsChunk& c, const Table& T
     // the lane's column of the LDS table, the stage bit of its length's first
     // value less 11 times its first code (n = 8, no match: not taken)
     const uint32_t G = gcol[64 * (n & 7u)];
+#if MYYUV_K5_FORMS
+    uint32_t vbit;  // (code < 2^8: v_mad_u32_u24; the compiler turns a 32-bit product + G into v_mad_u64_u32)
+    asm("v_mad_u32_u24 %0, %1, 11, %2" : "=v"(vbit) : "v"((uint32_t)(rwin >> 32) >> ((31u - n) & 31u)), "v"(G));
+#else
     const uint32_t vbit = ((uint32_t)(rwin >> 32) >> ((31u - n) & 31u)) * 11u + G;
+#endif
     const uint32_t P = take ? vbit : kZeroBit, w = P >> 5;  // (stage bits; kZeroBit: the zero quad)
     const uint32_t raw = funnel(c.st[w + 1], c.st[w], P);
     const uint32_t v = (uint32_t)(((int32_t)(raw << 21)) >> 21);

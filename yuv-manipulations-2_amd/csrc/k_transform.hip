@@ -146,6 +146,73 @@ __device__ __forceinline__ void store_block_rows(const uint32_t (&c)[16], uint32
   *(nzh ? dhi : sink + 64 + lane) = hi;
 }
 
+// K1's stores as buffer stores (1; 0: flat stores with per-lane pointers):
+// 32-bit offsets from wave-uniform descriptors, and a store that must not
+// happen (a zero row, a lane past the plane's end, a block left to the exact
+// path) gets an offset past the descriptor's range, which the hardware drops.
+// The flat form selects a sink pointer per store instead: two 64-bit selects
+// and a 64-bit add, each a VOP3 instruction (half the issue rate of the VOP2
+// forms on gfx950, tools/ubench/iforms.hip).  The launch's coefficient image
+// must stay below 4 GiB (make_geom / the batch split guarantee it).
+#ifndef MYYUV_K1_BUF
+#define MYYUV_K1_BUF 1
+#endif
+typedef unsigned int k1_v4u __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOob = 0xFFFFFFFFu;  // a buffer offset past every range: the store is dropped
+
+struct K1Rsrc {
+  __amdgpu_buffer_rsrc_t coef, rmask, binfo;
+};
+// descriptors of the launch's coefficient image, row masks and block words
+// (from kernel arguments only: wave-uniform)
+__device__ __forceinline__ K1Rsrc k1_rsrc(uint4* coef, uint8_t* rmask, uint32_t* binfo, const FrameGeom& G) {
+  const uint32_t nblk = G.cum[3] * G.nframes;
+  K1Rsrc r;
+  r.coef = __builtin_amdgcn_make_buffer_rsrc(coef, 0, (int)(((nblk + 63u) / 64u) * (kCoefQuadsPerWave * 16u)),
+                                             0x00020000);
+  r.rmask = __builtin_amdgcn_make_buffer_rsrc(rmask, 0, (int)nblk, 0x00020000);
+  r.binfo = __builtin_amdgcn_make_buffer_rsrc(binfo, 0, (int)(nblk * 4u), 0x00020000);
+  return r;
+}
+
+// store_block_rows through the descriptors: the same bytes, the skipped
+// stores dropped by an out-of-range offset instead of a sink
+__device__ __forceinline__ void store_block_rows_buf(const uint32_t (&c)[16], uint32_t q, bool live, uint32_t g,
+                                                     const K1Rsrc& R, const uint4* zq) {
+  uint4 lo, hi;
+  uint32_t rm;
+  pack_quads(c, q, lo, hi, rm);
+  const uint4 z0 = zq[0], z1 = zq[1];
+  const uint32_t wv[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t zv[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+  k1_us2 cnt = {0, 0}, mx = {0, 0};
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t fu, m16;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(fu) : "v"(wv[i]), "s"(0x00010001u));
+    cnt += __builtin_bit_cast(k1_us2, fu);
+    asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m16) : "v"(fu), "v"(zv[i]));
+    mx = __builtin_elementwise_max(mx, __builtin_bit_cast(k1_us2, m16));
+  }
+  uint32_t nnz = (uint32_t)cnt.x + (uint32_t)cnt.y;
+  uint32_t msz = mx.x > mx.y ? (uint32_t)mx.x : (uint32_t)mx.y;
+#pragma unroll
+  for (int d = 1; d < 4; d <<= 1) {
+    const uint32_t o = d == 1 ? quad_xor1(nnz | (msz << 16)) : quad_xor2(nnz | (msz << 16));
+    nnz += o & 0xFFFFu;
+    msz = max(msz, o >> 16);
+  }
+  const bool nzl = (rm >> (2 * q)) & 1u, nzh = (rm >> (2 * q + 1)) & 1u;
+  const uint32_t dc = quad_lane0(lo.x);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)rm, R.rmask, live ? g : kOob, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(binfo_word(rm, msz, class_of(nnz, msz), dc), R.binfo, live ? 4u * g : kOob,
+                                        0, 0);
+  const uint32_t qo = coef_quad(g, 2 * q) * 16u;  // quad 2q + 1 is 64 quads further
+  __builtin_amdgcn_raw_buffer_store_b128(k1_v4u{lo.x, lo.y, lo.z, lo.w}, R.coef, live && nzl ? qo : kOob, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(k1_v4u{hi.x, hi.y, hi.z, hi.w}, R.coef, live && nzh ? qo + 1024u : kOob, 0,
+                                         0);
+}
+
 // The zig-zag pair table in LDS (kZzPairs; before the tables' barrier)
 __device__ __forceinline__ void stage_zz(uint4* szz) {
   if (threadIdx.x < 32) reinterpret_cast<uint32_t*>(szz)[threadIdx.x] = kZzPairs.v[threadIdx.x];
@@ -182,6 +249,9 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
   const uint32_t q = lane & 3u, b = lane >> 2;  // quarter, block in the unit
   float* tb = tile[threadIdx.x >> 6] + b * kTile;
   uint8_t* img = reinterpret_cast<uint8_t*>(tb);  // the block's 8 x 8 B pixel image (aliases tb)
+#if MYYUV_K1_BUF
+  const K1Rsrc rs = k1_rsrc(coef, rmask, binfo, G);
+#endif
   // batch units: unit u of frame f is ua = f * ucum[3] + u
   const uint32_t nall = G.ucum[3] * G.nframes, stride = unit_stride();
   uint32_t ua = first_unit();
@@ -212,9 +282,13 @@ __global__ __launch_bounds__(256) MYYUV_K1_ATTR void k_fdct_quant(const uint8_t*
     // path, go to the sink (no branch: see load_rows)
     auto store = [&](const uint32_t (&c)[16], bool keep) {
       const bool lv = live && keep;
+#if MYYUV_K1_BUF
+      store_block_rows_buf(c, q, lv, g, rs, szz + 2 * q);
+#else
       uint4* dlo = lv ? coef + coef_quad(g, 2 * q) : sink + lane;
       uint4* dhi = lv ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
       store_block_rows(c, q, lane, lv, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
+#endif
     };
     uint32_t xr[4];
     fdct_load(img, q, xr);
@@ -272,6 +346,9 @@ __global__ __launch_bounds__(64 * kFixWaves) void k_fdct_fix(const uint8_t* __re
   float* tb = tile[threadIdx.x >> 6] + b * kTile;
   uint8_t* img = reinterpret_cast<uint8_t*>(tb);
   const uint32_t* list = fix_list(fix, G, c);
+#if MYYUV_K1_BUF
+  const K1Rsrc rs = k1_rsrc(coef, rmask, binfo, G);
+#endif
   for (uint32_t i = gw / kFixLists * kXfUnit; i < n; i += nw / kFixLists * kXfUnit) {
     // lanes past the list's end redo entry i (a real block) into the sink
     const bool real = i + b < n;
@@ -285,14 +362,18 @@ __global__ __launch_bounds__(64 * kFixWaves) void k_fdct_fix(const uint8_t* __re
     *reinterpret_cast<uint2*>(img + 16u * q) = make_uint2(r.x, r.y);
     *reinterpret_cast<uint2*>(img + 16u * q + 8u) = make_uint2(r.z, r.w);
     wave_sync();
-    uint4* dlo = real ? coef + coef_quad(g, 2 * q) : sink + lane;
-    uint4* dhi = real ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
     uint32_t xr[4];
     fdct_load(img, q, xr);
+#if MYYUV_K1_BUF
+    fdct_exact(xr, tb, q, sqr, U.p, [&](const uint32_t (&cc)[16]) { store_block_rows_buf(cc, q, real, g, rs, szz + 2 * q); });
+#else
+    uint4* dlo = real ? coef + coef_quad(g, 2 * q) : sink + lane;
+    uint4* dhi = real ? coef + coef_quad(g, 2 * q + 1) : sink + 64 + lane;
     fdct_exact(xr, tb, q, sqr, U.p,
                [&](const uint32_t (&cc)[16]) {
                  store_block_rows(cc, q, lane, real, g, dlo, dhi, rmask, binfo, szz + 2 * q, sink);
                });
+#endif
   }
 }
 
