@@ -444,6 +444,61 @@ def test_batch_decode_error_reports_frame(codec, oracle, golden):
     assert bad == nblk + single_bad
 
 
+def test_batch_split_into_launches(oracle, golden):
+    """A batch whose coefficient image would reach 4 GiB runs as several
+    launches (kMaxLaunchBlocks; here forced down to two 256x128 frames per
+    launch with MYYUV_LAUNCH_BLOCKS): 7 frames (launches of 2, 2, 2, 1) give
+    every frame's single-frame bytes, and a decode error in frame 5 names its
+    batch-global block, as one launch does."""
+    import torch
+    import malformed
+    import myyuv_hip
+    from conftest import _codec_with
+    w, h, q, n = 256, 128, (70, 60, 50), 7
+    nblk = (w // 8) * (h // 8) + 2 * (w // 16) * (h // 16)
+    frames = _batch_frames(golden, w, h, n)
+    c = _codec_with({"MYYUV_LAUNCH_BLOCKS": str(2 * nblk + 5)})
+    try:
+        fb = w * h * 3 // 2
+        cap = (myyuv_hip.payload_bound(w, h) + 3) & ~3
+        d_in = torch.frombuffer(bytearray(b"".join(frames)), dtype=torch.uint8).cuda()
+        d_pay = torch.zeros(n * cap, dtype=torch.uint8, device="cuda")
+        d_sizes = torch.zeros(n, dtype=torch.int32, device="cuda")
+        d_out = torch.empty(n * fb, dtype=torch.uint8, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        c.compress_batch_device(d_in.data_ptr(), n, w, h, q, d_pay.data_ptr(), cap, d_sizes.data_ptr(), stream)
+        c.decompress_batch_device(d_pay.data_ptr(), d_sizes.data_ptr(), cap, n, w, h, q, d_out.data_ptr(), stream)
+        rc, bad = c.sync_status(stream)
+        assert rc == 0, (rc, bad)
+        pay, out, sizes = d_pay.cpu().numpy(), d_out.cpu().numpy(), d_sizes.cpu().numpy()
+        pays = []
+        for f in range(n):
+            exp = oracle.compress(frames[f], w, h, q)
+            pays.append(exp)
+            assert bytes(pay[f * cap: f * cap + int(sizes[f])]) == exp, f
+            assert bytes(out[f * fb:(f + 1) * fb]) == oracle.decompress(exp, w, h, q), f
+        # a malformed stream as frame 5 (the third launch)
+        _, badpay = next((nm, p) for nm, p, kind in malformed.cases(pays[5]) if nm == "bad_code")
+        with pytest.raises(myyuv_hip.CodecError) as single:
+            c.decompress(badpay, w, h, q)
+        assert single.value.bad_block >= 0
+        cap2 = (max(len(p) for p in pays + [badpay]) + 3) & ~3
+        buf = bytearray(n * cap2)
+        lens = []
+        for f in range(n):
+            p = badpay if f == 5 else pays[f]
+            buf[f * cap2: f * cap2 + len(p)] = p
+            lens.append(len(p))
+        d_pay2 = torch.frombuffer(buf, dtype=torch.uint8).cuda()
+        d_sz2 = torch.tensor(lens, dtype=torch.int32, device="cuda")
+        c.decompress_batch_device(d_pay2.data_ptr(), d_sz2.data_ptr(), cap2, n, w, h, q, d_out.data_ptr(), stream)
+        rc, bad = c.sync_status(stream)
+        assert rc == single.value.code
+        assert bad == 5 * nblk + single.value.bad_block
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("cap", [8, 64, 4096, 100000])
 def test_device_compress_capacity_is_respected(codec, golden, oracle, cap):
     """compress_device into a slot smaller than the payload: MYYUV_E_CAPACITY,

@@ -122,7 +122,14 @@ struct FrameGeom {
   // a plane may be shorter), cumulative per plane; tile t of frame f is
   // batch tile f * tcum[3] + t
   uint32_t tcum[4];
+  // index of frame 0 of this launch in the caller's batch (a batch whose
+  // coefficient image would reach 4 GiB runs as several launches, kMaxLaunchBlocks):
+  // only the error keys use it, which name batch-global blocks
+  uint32_t fbase;
 };
+// Blocks per launch: the coefficient image (128 B per block, in 64-block
+// groups) stays below 4 GiB, the range of the kernels' 32-bit buffer offsets.
+constexpr uint32_t kMaxLaunchBlocks = (1u << 25) - 64u;
 
 // floor(x / d) for a 32-bit x from m = ceil(2^64 / d) (m = 0 for d = 1): the
 // product overshoots x / d by less than x / 2^64, below the 1 / d slack.

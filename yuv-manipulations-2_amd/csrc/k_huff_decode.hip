@@ -90,10 +90,6 @@ __device__ __forceinline__ void record_error(unsigned long long* err, uint64_t k
   atomicMin(err, (unsigned long long)((key << 8) | (uint64_t)code));
 }
 
-__device__ __forceinline__ uint32_t scanned(const uint32_t* local_off, const uint32_t* tile_pre,
-                                            uint32_t g) {
-  return local_off[g] + tile_pre[g / kScanTile];
-}
 
 // Inclusive sum over the wave's 64 lanes by DPP (rows of 16 by row_shr 1, 2,
 // 4, 8, then row_bcast 15 / 31 across rows; lanes whose source is out of
@@ -473,7 +469,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   // the chunks must fit the declared content.
   bool ok = live && !bad;
   if (ok && rel + s > csize) {
-    record_error(err, 2ull * (gbase + cum_p), 9 /* MYYUV_E_PLANE_CONTENT */);
+    record_error(err, 2ull * ((uint64_t)G.fbase * nblk + gbase + cum_p), 9 /* MYYUV_E_PLANE_CONTENT */);
     ok = false;
   }
 
@@ -545,7 +541,7 @@ __device__ __forceinline__ bool decode_group(const uint8_t* __restrict__ in, con
   // ends, whether or not a round ran (no lane ok: round 1's loads were still
   // issued)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (ok && code) record_error(err, 2ull * (gbase + g) + 1, code);
+  if (ok && code) record_error(err, 2ull * ((uint64_t)G.fbase * nblk + gbase + g) + 1, code);
   D.f = f;
   D.gbase = gbase;
   D.g0 = g0;

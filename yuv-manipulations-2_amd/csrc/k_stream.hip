@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void k_scan_chain(const uint8_t* __restrict__ 
     if (code) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         desc->bad = 1;
-        record_error(err, 2ull * f * G.cum[3], code);  // frame f's first block (0: header of frame 0)
+        record_error(err, 2ull * (G.fbase + f) * G.cum[3], code);  // frame f's first block (0: header of frame 0)
       }
       return;
     }

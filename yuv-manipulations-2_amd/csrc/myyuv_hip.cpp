@@ -165,7 +165,17 @@ int make_geom(uint32_t w, uint32_t h, FrameGeom& G) {
   G.nframes = 1;
   G.fbytes = w * h / 2 * 3;
   G.umag = block_magic(G.ucum[3]);
+  G.fbase = 0;
+  // one frame's coefficient image within the kernels' 32-bit offsets (> 1.4 G
+  // pixels; the reference's getImageSize overflows from 537 M pixels)
+  if (G.cum[3] > kMaxLaunchBlocks) return MYYUV_E_ARG;
   return 0;
+}
+
+// Frames per launch of geometry G (kMaxLaunchBlocks, or a smaller
+// diagnostic cap: MYYUV_LAUNCH_BLOCKS, read at context creation).
+uint32_t launch_frames(const FrameGeom& G, uint32_t cap_blocks = kMaxLaunchBlocks) {
+  return std::max(1u, std::min(cap_blocks, kMaxLaunchBlocks) / G.cum[3]);
 }
 
 // A batch of nf frames of G's geometry (block, unit and byte counts of the
@@ -209,6 +219,7 @@ struct myyuv_hip_ctx {
   // can list far more units than the bench frame's 0.07 %.
   uint32_t fix_grid = 0;
   uint32_t fix_qmax = 75;  // (MYYUV_FIX_QMAX)
+  uint32_t launch_blocks = kMaxLaunchBlocks;  // blocks per launch (MYYUV_LAUNCH_BLOCKS: a test of the batch split)
   // encoder: K1 -> K2 through HBM (split), or the fused single-pass kernel
   // k_encode_tile (MYYUV_ENCODER=fused|split)
   bool fused = false;
@@ -687,6 +698,8 @@ int myyuv_hip_create(int device, myyuv_hip_handle* out) {
         c->fix_resident = (uint32_t)(cus * nfix) * kFixWaves / 4;  // (in 4-wave workgroups)
       if (const char* v = std::getenv("MYYUV_FIX_GRID")) c->fix_grid = (uint32_t)std::atoi(v);
       if (const char* v = std::getenv("MYYUV_FIX_QMAX")) c->fix_qmax = (uint32_t)std::atoi(v);
+      if (const char* v = std::getenv("MYYUV_LAUNCH_BLOCKS"))
+        c->launch_blocks = std::max(1u, std::min(kMaxLaunchBlocks, (uint32_t)std::strtoul(v, nullptr, 10)));
       {
         const char* v = std::getenv("MYYUV_ENCODER");
         c->fused = v && std::strcmp(v, "fused") == 0;
@@ -766,8 +779,19 @@ int myyuv_gpu_dct_compress_batch_device(myyuv_hip_handle c, const void* d_in, ui
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
   StreamOrder so(c, s);
-  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
-  return launch_compress(c, G, d_in, d_out, cap, d_sizes, s);
+  // (as several launches when the batch's coefficient image would reach 4 GiB)
+  const uint32_t per = launch_frames(G, c->launch_blocks);
+  FrameGeom GL = G;
+  if ((e = set_batch(GL, std::min(nframes, per))) || (e = reserve(c, GL)) || (e = set_qtables(c, q, s))) return e;
+  for (uint32_t f0 = 0; f0 < nframes; f0 += per) {
+    GL = G;
+    GL.fbase = f0;
+    if ((e = set_batch(GL, std::min(per, nframes - f0))) ||
+        (e = launch_compress(c, GL, static_cast<const uint8_t*>(d_in) + (size_t)f0 * G.fbytes,
+                             static_cast<uint8_t*>(d_out) + (size_t)f0 * cap, cap, d_sizes + f0, s)))
+      return e;
+  }
+  return 0;
 }
 
 int myyuv_gpu_dct_decompress_batch_device(myyuv_hip_handle c, const void* d_in, const uint32_t* d_sizes,
@@ -785,8 +809,18 @@ int myyuv_gpu_dct_decompress_batch_device(myyuv_hip_handle c, const void* d_in, 
   DeviceGuard g(c->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
   StreamOrder so(c, s);
-  if ((e = reserve(c, G)) || (e = set_qtables(c, q, s))) return e;
-  return launch_decompress(c, G, d_in, d_sizes, cap, d_out, s);
+  const uint32_t per = launch_frames(G, c->launch_blocks);
+  FrameGeom GL = G;
+  if ((e = set_batch(GL, std::min(nframes, per))) || (e = reserve(c, GL)) || (e = set_qtables(c, q, s))) return e;
+  for (uint32_t f0 = 0; f0 < nframes; f0 += per) {
+    GL = G;
+    GL.fbase = f0;
+    if ((e = set_batch(GL, std::min(per, nframes - f0))) ||
+        (e = launch_decompress(c, GL, static_cast<const uint8_t*>(d_in) + (size_t)f0 * cap, d_sizes + f0, cap,
+                               static_cast<uint8_t*>(d_out) + (size_t)f0 * G.fbytes, s)))
+      return e;
+  }
+  return 0;
 }
 
 int myyuv_gpu_dct_compress_device(myyuv_hip_handle c, const void* d_in, uint32_t w, uint32_t h,
@@ -807,6 +841,7 @@ int myyuv_hip_reserve_batch(myyuv_hip_handle c, uint32_t w, uint32_t h, uint32_t
   int e = make_geom(w, h, G);
   if (e || (e = set_batch(G, nframes))) return e;
   std::lock_guard<std::mutex> lk(c->mu);
+  if ((e = set_batch(G, std::min(nframes, launch_frames(G, c->launch_blocks))))) return e;  // (the largest launch)
   DeviceGuard g(c->device);
   return reserve(c, G);
 }
@@ -1056,7 +1091,7 @@ int compress_frames(myyuv_hip_ctx* c, const uint8_t* const* frames, uint32_t nf,
   if (e) return e;
   const size_t fb = (size_t)w * h * 3 / 2;
   const uint32_t dcap = (myyuv_dct_payload_bound(w, h) + 3) & ~3u;  // device slot per frame
-  const uint32_t B = pipe_chunk(nf, fb + dcap);
+  const uint32_t B = std::min(pipe_chunk(nf, fb + dcap), launch_frames(G, c->launch_blocks));
   FrameGeom GB = G;
   if ((e = set_batch(GB, B))) return e;
   hipStream_t s = c->stream;
@@ -1129,7 +1164,7 @@ int decompress_frames(myyuv_hip_ctx* c, const uint8_t* const* payloads, const ui
   const size_t fb = (size_t)w * h * 3 / 2;
   uint32_t icap = 4;  // device slot per stream: the longest, 4-aligned
   for (uint32_t f = 0; f < nf; f++) icap = std::max(icap, (psizes[f] + 3u) & ~3u);
-  const uint32_t B = pipe_chunk(nf, fb + icap);
+  const uint32_t B = std::min(pipe_chunk(nf, fb + icap), launch_frames(G, c->launch_blocks));
   FrameGeom GB = G;
   if ((e = set_batch(GB, B))) return e;
   hipStream_t s = c->stream;
