@@ -49,8 +49,9 @@ order at N = 1).
 roofline: K1 fdct_quant, the block-transform kernel of the north star.
 Algorithmic bytes = 3 B per sample (1 B u8 in + 2 B int16 out)
 x the samples of the launches; time = those launches' HIP-event durations,
-K1's own plus those of k_fdct_fix (K1's exact path for the units whose fast
-result it cannot prove; it runs right after K1 in the stream)
+K1's own; k_fdct_fix (K1's exact path for the blocks whose fast result it
+cannot prove; it runs right after K1 in the stream) is stamped as well and
+reported beside it, with the fraction of K1 + fix summed (`fix_kernel`)
 (dispatch-stamped on their streams, every launch group's K1 by default,
 --events-ctx0: group 0's only) over the timed region, where K1 shares the GPU
 with the other groups in flight.  `traffic` = calibrated FETCH_SIZE/WRITE_SIZE
@@ -58,8 +59,8 @@ bytes per launch from the newest rocprofv3 --pmc profile of this workload
 under profiles/ (null if none); `traffic_gbs` = traffic / avg launch time.
 K1 is VALU-issue bound: `valu_ceiling_frac` is the fraction of
 the HBM peak its fast path's instructions alone allow (the gfx950 code object's
-VALU count per 16-block unit at the 2-cycle f32 issue rate on 1,024 SIMDs at
-the effective clock), so `frac` reads against it.  roofline_isolated: the
+loop body weighted by the measured issue cost of each instruction form,
+K1_ISSUE_NS_PER_UNIT, on 1,024 SIMDs), so `frac` reads against it.  roofline_isolated: the
 same K1 figure from the untimed one-group-at-a-time breakdown pass.
 
 cpu_baseline (rank 0, N = 1): the reference library itself (oracle/_ref,
@@ -109,15 +110,15 @@ BIG_DECODED_SHA = "5e7769191188285cc127c6b4da900b3420f064191f707383c82128c14e497
 BIG_RECOMPRESSED_SHA = "fe9b7317653c2b44a9f24436f0e349b083b4e368cf9653e8777e9f7a79cebfcc"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8 TB/s spec)
 SLOT_4K = 4 << 20  # batch4k payload slot: the largest of the 512 streams is 2,471,404 B (capacity is checked on device)
-# K1's VALU work (the gfx950 code object's loop body): VALU
-# instructions per lane per 16-block unit on the fast path (round 5's
-# butterflies: 409, with the ~60 of the block words K1 writes for K2's
-# classification; round 4's FMA chains ~550, round 3's reference order 660);
-# f32 VALU issue = 2 cycles per wave-instruction (64 lanes on a 32-wide
-# SIMD), 1,024 SIMDs, effective clock under load from GRBM_GUI_ACTIVE
-# (profiles/r02b_sq_counters.txt)
-K1_VALU_PER_UNIT = 409
-K1_CLOCK_GHZ = 1.7
+# K1's VALU issue time: the fast path's loop body in the
+# gfx950 code object of this build, weighted by the issue cost of each
+# instruction form measured on MI355X at 8 waves per SIMD (tools/ubench/
+# vforms.hip, iforms.hip; profiles/r6g_iforms_and_k5_forms.txt): 1.0 ns per
+# wave-instruction per SIMD for the VOP2/VOP1 forms and f32 mul/add/fma,
+# 1.8 ns for VOP3-only integer forms, compares, conversions, SDWA, DPP and
+# packed forms.  Round 6: 246 fast + 131 slow instructions per lane-unit
+# (round 5's flat stores: 254 + 144)
+K1_ISSUE_NS_PER_UNIT = 246 * 1.0 + 131 * 1.8
 
 
 def log(*a):
@@ -827,11 +828,10 @@ def k1_roofline(stats, samples_per_frame, frames, B, frame_key):
 
 
 def valu_ceiling_frac(samples_per_frame):
-    """The HBM fraction K1's VALU issue alone allows: per 16-block unit (1,024
-    samples, 3,072 algorithmic bytes) each of its 64 lanes issues
-    K1_VALU_PER_UNIT instructions; a wave-instruction takes 2 cycles on a
-    32-wide SIMD; 1,024 SIMDs at K1_CLOCK_GHZ."""
-    unit_s = K1_VALU_PER_UNIT * 2 / (K1_CLOCK_GHZ * 1e9) / 1024  # seconds of the whole chip per unit
+    """The HBM fraction K1's VALU issue alone allows: a 16-block unit (1,024
+    samples, 3,072 algorithmic bytes) occupies one SIMD's VALU issue for
+    K1_ISSUE_NS_PER_UNIT ns; 1,024 SIMDs."""
+    unit_s = K1_ISSUE_NS_PER_UNIT * 1e-9 / 1024  # seconds of the whole chip per unit
     return round(3 * 1024 / unit_s / 1e9 / HBM_PEAK_GBS, 4)
 
 
