@@ -32,12 +32,34 @@
 #define LSHLOR(i) "v_lshl_or_b32 v" #i ", v" #i ", 16, v40\n"
 #define BFEU(i) "v_bfe_u32 v" #i ", v" #i ", 8, 8\n"
 #define CMPX(i) "v_cmp_lt_u32 vcc, v" #i ", v40\n"
-#define CLOB "v0","v1","v2","v3","v4","v5","v6","v7","v8","v9","v10","v11","v12","v13","v14","v15","v40","v41","s42","s43","vcc"
+#define CNDV(i) "v_cndmask_b32_e32 v" #i ", v" #i ", v40, vcc\n"
+#define BITOP3(i) "v_bitop3_b32 v" #i ", v" #i ", v40, v41 bitop3:0xc8\n"
+#define BFI(i) "v_bfi_b32 v" #i ", v" #i ", v40, v41\n"
+#define MAXU(i) "v_max_u32 v" #i ", v" #i ", v40\n"
+#define CVTUB(i) "v_cvt_f32_ubyte1 v" #i ", v" #i "\n"
+#define FRACT(i) "v_fract_f32 v" #i ", v" #i "\n"
+#define RNDNE(i) "v_rndne_f32 v" #i ", v" #i "\n"
+#define MED3(i) "v_med3_f32 v" #i ", v" #i ", v40, v41\n"
+#define CMPROT(i) "v_cmp_lt_u32_e64 s[" #i "*2+40:" #i "*2+41], v" #i ", v40\n"
+#define XOR(i) "v_xor_b32 v" #i ", v" #i ", v40\n"
+#define MULHI24(i) "v_mul_hi_u32_u24 v" #i ", v" #i ", v40\n"
+#define ASHR(i) "v_ashrrev_i32 v" #i ", v40, v" #i "\n"
+#define SUBREV(i) "v_subrev_u32 v" #i ", v" #i ", v40\n"
+#define CMPCLASS(i) "v_cmp_class_f32_e64 s[42:43], v" #i ", v40\n"
+#define MAXF(i) "v_max_f32 v" #i ", v" #i ", v40\n"
+#define MINF(i) "v_min_f32 v" #i ", v" #i ", v40\n"
+#define ANDV(i) "v_and_b32 v" #i ", v" #i ", v40\n"
+#define ORV(i) "v_or_b32 v" #i ", v" #i ", v40\n"
+#define ADDCO(i) "v_add_co_u32 v" #i ", vcc, v" #i ", v40\n"
+#define SELPAIR(i) "v_cmp_lt_u32 vcc, v" #i ", v40\n v_cndmask_b32 v" #i ", v" #i ", v41, vcc\n"
+#define MAXI(i) "v_max_i32 v" #i ", v" #i ", v40\n"
+#define MINU(i) "v_min_u32 v" #i ", v" #i ", v40\n"
+#define CLOB "v0","v1","v2","v3","v4","v5","v6","v7","v8","v9","v10","v11","v12","v13","v14","v15","v40","v41","s42","s43","vcc","s40","s41","s44","s45","s46","s47","s48","s49","s50","s51","s52","s53","s54","s55","s56","s57","s58","s59","s60","s61","s62","s63","s64","s65","s66","s67","s68","s69","s70","s71"
 
-constexpr int kN = 21;
+constexpr int kN = 43;
 template <int K>
 __global__ __launch_bounds__(256) void kern(unsigned* out, int iters) {
-  asm volatile("v_mov_b32 v40, 3\n v_mov_b32 v41, 5\n s_mov_b64 s[44:45], exec\n" ::: "v40", "v41", "s44", "s45");
+  asm volatile("v_mov_b32 v40, 3\n v_mov_b32 v41, 5\n s_mov_b64 s[44:45], exec\n s_mov_b64 vcc, exec\n" ::: "v40", "v41", "s44", "s45", "vcc");
   for (int it = 0; it < iters; it++) {
     if (K == 0) asm volatile(B16(ADD) ::: CLOB);
     if (K == 1) asm volatile(B8P(MAD64) ::: CLOB);
@@ -60,6 +82,28 @@ __global__ __launch_bounds__(256) void kern(unsigned* out, int iters) {
     if (K == 18) asm volatile(B16(LSHLOR) ::: CLOB);
     if (K == 19) asm volatile(B16(BFEU) ::: CLOB);
     if (K == 20) asm volatile(B16(CMPX) ::: CLOB);
+    if (K == 21) asm volatile(B16(CNDV) ::: CLOB);
+    if (K == 22) asm volatile(B16(BITOP3) ::: CLOB);
+    if (K == 23) asm volatile(B16(BFI) ::: CLOB);
+    if (K == 24) asm volatile(B16(MAXU) ::: CLOB);
+    if (K == 25) asm volatile(B16(CVTUB) ::: CLOB);
+    if (K == 26) asm volatile(B16(FRACT) ::: CLOB);
+    if (K == 27) asm volatile(B16(RNDNE) ::: CLOB);
+    if (K == 28) asm volatile(B16(MED3) ::: CLOB);
+    if (K == 29) asm volatile(B16(CMPROT) ::: CLOB);
+    if (K == 30) asm volatile(B16(XOR) ::: CLOB);
+    if (K == 31) asm volatile(B16(MULHI24) ::: CLOB);
+    if (K == 32) asm volatile(B16(ASHR) ::: CLOB);
+    if (K == 33) asm volatile(B16(SUBREV) ::: CLOB);
+    if (K == 34) asm volatile(B16(CMPCLASS) ::: CLOB);
+    if (K == 35) asm volatile(B16(MAXF) ::: CLOB);
+    if (K == 36) asm volatile(B16(MINF) ::: CLOB);
+    if (K == 37) asm volatile(B16(ANDV) ::: CLOB);
+    if (K == 38) asm volatile(B16(ORV) ::: CLOB);
+    if (K == 39) asm volatile(B16(ADDCO) ::: CLOB);
+    if (K == 40) asm volatile(B16(SELPAIR) ::: CLOB);
+    if (K == 41) asm volatile(B16(MAXI) ::: CLOB);
+    if (K == 42) asm volatile(B16(MINU) ::: CLOB);
   }
   out[blockIdx.x * 256 + threadIdx.x] = 1u;
 }
@@ -82,15 +126,27 @@ int main() {
   (void)hipEventCreate(&e1);
   const Fn fns[kN] = {launch<0>,  launch<1>,  launch<2>,  launch<3>,  launch<4>,  launch<5>,  launch<6>,
                       launch<7>,  launch<8>,  launch<9>,  launch<10>, launch<11>, launch<12>, launch<13>,
-                      launch<14>, launch<15>, launch<16>, launch<17>, launch<18>, launch<19>, launch<20>};
+                      launch<14>, launch<15>, launch<16>, launch<17>, launch<18>, launch<19>, launch<20>,
+                      launch<21>, launch<22>, launch<23>, launch<24>, launch<25>, launch<26>, launch<27>,
+                      launch<28>, launch<29>, launch<30>, launch<31>, launch<32>, launch<33>, launch<34>,
+                      launch<35>, launch<36>, launch<37>, launch<38>, launch<39>, launch<40>, launch<41>,
+                      launch<42>};
   const char* names[kN] = {"v_add_u32 (VOP2)",        "v_mad_u64_u32",        "v_mad_u32_u24",
                            "v_mul_u32_u24 (VOP2)",    "v_mul_u32_u24_sdwa",   "v_lshlrev_b64",
                            "v_alignbit_b32",          "v_bcnt_u32_b32",       "v_cmp_lt_u32_sdwa -> s[]",
                            "v_cmp_lt_u32_e64 -> s[]", "v_and_or_b32",         "v_add3_u32",
                            "v_cndmask_b32_e64 s[]",   "v_mul_lo_u32",         "v_lshrrev_b32 (VOP2)",
                            "v_min_u32_sdwa",          "v_pk_add_u16",         "v_mov_b32_dpp quad_perm",
-                           "v_lshl_or_b32",           "v_bfe_u32",            "v_cmp_lt_u32_e32 -> vcc"};
-  for (int wps : {4, 8}) {
+                           "v_lshl_or_b32",           "v_bfe_u32",            "v_cmp_lt_u32_e32 -> vcc",
+                           "v_cndmask_b32_e32 (vcc)", "v_bitop3_b32",         "v_bfi_b32",
+                           "v_max_u32 (VOP2)",        "v_cvt_f32_ubyte1",     "v_fract_f32",
+                           "v_rndne_f32",             "v_med3_f32",           "v_cmp_lt_u32_e64 rot s[]",
+                           "v_xor_b32 (VOP2)",        "v_mul_hi_u32_u24",     "v_ashrrev_i32 (VOP2)",
+                           "v_subrev_u32 (VOP2)",     "v_cmp_class_f32_e64",  "v_max_f32 (VOP2)",
+                           "v_min_f32 (VOP2)",        "v_and_b32 (VOP2)",     "v_or_b32 (VOP2)",
+                           "v_add_co_u32 -> vcc",     "cmp->vcc + cndmask (per pair)", "v_max_i32 (VOP2)",
+                           "v_min_u32 (VOP2)"};
+  for (int wps : {8}) {
     for (int k = 0; k < kN; k++) {
       const int iters = 512;
       float best = 1e9;
@@ -103,7 +159,7 @@ int main() {
         (void)hipEventElapsedTime(&ms, e0, e1);
         if (ms < best) best = ms;
       }
-      const double insts = (double)iters * 64 * wps;
+      const double insts = (double)iters * (k == 40 ? 128 : 64) * wps;
       printf("waves/SIMD %d %-26s %.3f ns/inst/SIMD\n", wps, names[k], best * 1e6 / insts);
     }
   }
