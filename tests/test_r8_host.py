@@ -143,11 +143,13 @@ def test_dense_run_matches_concatenated_chunks(harness, oracle):
     assert out[4:] == want
 
 
-def check16(exe, oracle, nat):
+def check16(exe, oracle, nat, mode="16"):
     """The CAP-16 tier (huff_r16.hpp build_r16 + emit_chunk16): the oracle's
-    chunk for every block with at most 16 distinct symbols, declined above."""
+    chunk for every block with at most 16 distinct symbols, declined above.
+    mode "16": the register heap (r16::RegHeap16); "16l": the kernel's
+    LDS-column heap (r16::LdsHeap16) over a local column."""
     nat = np.asarray(nat, np.int16).reshape(-1, 64)
-    got = run(exe, nat, "16")
+    got = run(exe, nat, mode)
     n_ok = 0
     for x, ch in zip(nat, got):
         msg = x[ZZ]
@@ -161,7 +163,11 @@ def check16(exe, oracle, nat):
     return n_ok
 
 
-def test_r16_rehash_boundaries(harness, oracle):
+HEAPS = pytest.mark.parametrize("heap", ["16", "16l"])
+
+
+@HEAPS
+def test_r16_rehash_boundaries(harness, oracle, heap):
     """12..16 distinct symbols, with and without a zero inside the message,
     with and without trailing zeros: the map's rehash to 29 buckets before
     the 14th key, or before the freq[0] probe inserts key 0 into a 13-key map
@@ -185,10 +191,11 @@ def test_r16_rehash_boundaries(harness, oracle):
                     x = np.zeros(64, np.int16)
                     x[ZZ[:m]] = msg
                     nat.append(x)
-    assert check16(harness, oracle, nat) == len(nat)
+    assert check16(harness, oracle, nat, heap) == len(nat)
 
 
-def test_r16_random_and_edge_blocks(harness, oracle):
+@HEAPS
+def test_r16_random_and_edge_blocks(harness, oracle, heap):
     rng = np.random.default_rng(17)
     nat = np.zeros((6000, 64), np.int16)
     for x in nat:
@@ -202,10 +209,11 @@ def test_r16_random_and_edge_blocks(harness, oracle):
         x = np.zeros(64, np.int16)
         x[ZZ] = b
         edge.append(x)
-    assert check16(harness, oracle, np.concatenate([nat, np.array(edge)])) > 4000
+    assert check16(harness, oracle, np.concatenate([nat, np.array(edge)]), heap) > 4000
 
 
-def test_r16_golden_frame_blocks(harness, oracle, golden):
+@HEAPS
+def test_r16_golden_frame_blocks(harness, oracle, golden, heap):
     f = golden("chef-with-trumpet-big-DCT-50.myyuv")
     raw = np.frombuffer(oracle.decompress(f.data, f.width, f.height, tuple(f.params)), np.uint8)
     w, h = f.width, f.height
@@ -215,7 +223,7 @@ def test_r16_golden_frame_blocks(harness, oracle, golden):
     for q in (50, 90, 100):
         Q = oracle.qtable(q, 0)
         nat = np.stack([oracle.fdct_block(y[i], Q) for i in pick])
-        assert check16(harness, oracle, nat) > 1900
+        assert check16(harness, oracle, nat, heap) > 1900
 
 
 def test_sanitized_host_build_is_clean(harness, harness_san, oracle):

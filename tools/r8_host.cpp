@@ -69,7 +69,9 @@ int main(int argc, char** argv) {
       for (int w = 0; w < 32; w++)
         R.w[w] = (uint16_t)c[b * 64 + 2 * w] | ((uint32_t)(uint16_t)c[b * 64 + 2 * w + 1] << 16);
       EncState16 S16;
-      const bool ok16 = build_r16(R, R.msz(), 64, S16);
+      uint32_t col[16] = {0};  // "16l": the kernel's LDS-column heap over a local column
+      const bool ok16 = mode[2] == 'l' ? build_r16(R, R.msz(), 64, S16, r16::LdsHeap16<1>{col})
+                                       : build_r16(R, R.msz(), 64, S16);
       const uint8_t hdr[2] = {(uint8_t)ok16, ok16 ? (uint8_t)S16.size : (uint8_t)0};
       fwrite(hdr, 1, 2, stdout);
       if (ok16) {

@@ -218,6 +218,63 @@ MYYUV_HD uint32_t pop16(uint32_t (&H)[16], uint32_t m) {
   return top;
 }
 
+// The heap of build_r16 on 16 registers (push16 / pop16): the host build
+// and the reference for LdsHeap16.
+struct RegHeap16 {
+  uint32_t H[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  MYYUV_HD void push(uint32_t h, uint32_t e) { push16(H, h, e); }
+  MYYUV_HD uint32_t pop(uint32_t m) { return pop16(H, m); }
+};
+
+// The same heap as a column of LDS per lane: entry k of lane l's heap at
+// word k * S + l.  Every access of a wave is conflict-free whatever each
+// lane's k (bank = lane), so the walks are plain per-lane loops (libstdc++'s
+// __push_heap / __adjust_heap, strict comparisons on the freq), one LDS
+// round trip per level, instead of push16 / pop16's selects over all 16
+// positions at every step (425 / 975 instructions per push / merge step).
+template <uint32_t S>
+struct LdsHeap16 {
+  uint32_t* c;  // &lds[lane]
+  MYYUV_HD uint32_t& at(uint32_t k) const { return c[k * S]; }
+  // __push_heap(first, hole h, top 0, e): parents whose freq exceeds e's move down
+  MYYUV_HD void push(uint32_t h, uint32_t e) const {
+    const uint32_t eh = e | 0xFFu;
+    uint32_t hole = h;
+    while (hole > 0) {
+      const uint32_t p = (hole - 1u) >> 1;
+      const uint32_t pe = at(p);
+      if (pe <= eh) break;
+      at(hole) = pe;
+      hole = p;
+    }
+    at(hole) = e;
+  }
+  // pop_heap of a heap of m + 1 entries: __adjust_heap(first, 0, m, last),
+  // then __push_heap of the old last entry from the hole
+  MYYUV_HD uint32_t pop(uint32_t m) const {
+    const uint32_t top = at(0);
+    if (m == 0) return top;  // (one entry: nothing moves)
+    const uint32_t v = at(m);
+    uint32_t hole = 0, child = 0;
+    const uint32_t lim = (m - 1u) >> 1;
+    while (child < lim) {
+      child = 2u * (child + 1u);
+      const uint32_t r = at(child), l = at(child - 1u);
+      const bool left = fq_gt(r, l);
+      child -= left ? 1u : 0u;
+      at(hole) = left ? l : r;
+      hole = child;
+    }
+    if ((m & 1u) == 0 && child == (m - 2u) >> 1) {
+      child = 2u * (child + 1u);
+      at(hole) = at(child - 1u);
+      hole = child - 1u;
+    }
+    push(hole, v);
+    return top;
+  }
+};
+
 }  // namespace r16
 
 // What emit_chunk16 needs of a block whose code was built by build_r16.
@@ -230,8 +287,10 @@ struct EncState16 {
   SlotIds<16> ids;   // per position: slot of its symbol
 };
 
-// Returns false when the block has more than 16 distinct symbols.
-MYYUV_HD bool build_r16(const CoefRegs& R, int msz, int wave_msz, EncState16& S) {
+// Returns false when the block has more than 16 distinct symbols.  Heap:
+// r16::RegHeap16 or (device) r16::LdsHeap16.
+template <class Heap = r16::RegHeap16>
+MYYUV_HD bool build_r16(const CoefRegs& R, int msz, int wave_msz, EncState16& S, Heap hp = Heap()) {
   using namespace r16;
   // ---------------- 1. distinct symbols, counts, per-position slots ----------------
   uint32_t KP[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // tagged keys, field k = slot k
@@ -321,27 +380,24 @@ MYYUV_HD bool build_r16(const CoefRegs& R, int msz, int wave_msz, EncState16& S)
     walk16(it, ord, rank);
   }
   // ---------------- 3. Huffman merges on the libstdc++ heap ----------------
-  uint32_t H[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) H[k] = 0;
 #pragma unroll 1
   for (uint32_t r = 0; r < n; r++) {
     const uint32_t k = nib(ord, r);
     const uint32_t cv = (uint32_t)(((k & 8u) ? cnt1 : cnt0) >> (8 * (k & 7u))) & 0xFFu;
-    push16(H, r, (cv << 8) | k);
+    hp.push(r, (cv << 8) | k);
   }
   uint64_t lpar = 0, ipar = 0;  // parent (merge index) of leaf k / internal j, nibbles
 #pragma unroll 1
   for (uint32_t j = 0; j + 1 < n; j++) {
-    const uint32_t l = pop16(H, n - 1 - j);
-    const uint32_t r = pop16(H, n - 2 - j);
+    const uint32_t l = hp.pop(n - 1 - j);
+    const uint32_t r = hp.pop(n - 2 - j);
 #pragma unroll
     for (int s = 0; s < 2; s++) {
       const uint32_t id = (s == 0 ? l : r) & 0xFFu;
       if (id < 16) nib_set(lpar, id, j);
       else nib_set(ipar, id - 16, j);
     }
-    push16(H, n - 2 - j, ((rr::fq(l) + rr::fq(r)) << 8) | (16u + j));
+    hp.push(n - 2 - j, ((rr::fq(l) + rr::fq(r)) << 8) | (16u + j));
   }
   // depths of internal nodes (root = n - 2 at depth 0), then code lengths
   uint64_t dep = 0;

@@ -1462,6 +1462,9 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
 // register program per block instead of the LDS replay's chain of dependent
 // round trips (8192^2 q90: 214 -> 145 us with the wave pass on work2,
 // profiles/r3t_*).
+#ifndef MYYUV_R16_LDS
+#define MYYUV_R16_LDS 1  // the heap in LDS (r16::LdsHeap16) rather than registers (r16::RegHeap16)
+#endif
 #ifndef MYYUV_R16_WAVES
 #define MYYUV_R16_WAVES 5  // waves per SIMD k_huff_encode_r16 is compiled for: 96 VGPRs, 8 spilled (3 waves at 131: -1.5 %, profiles/r3zzl_*)
 #endif
@@ -1478,6 +1481,12 @@ __global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const u
   const uint32_t cnt = *work_count;
   if (cnt <= kR16Gate) return;  // one CAP-64 round takes the list
   const uint32_t lane = threadIdx.x;
+#if MYYUV_R16_LDS
+  __shared__ uint32_t heap[16 * kWave];  // the lanes' heaps, one LDS column each
+  const r16::LdsHeap16<kWave> hp{heap + lane};
+#else
+  const r16::RegHeap16 hp;
+#endif
   for (uint32_t base = blockIdx.x * kWave; base < cnt; base += gridDim.x * kWave) {
     const uint32_t i = base + lane;
     const bool live = i < cnt;
@@ -1487,7 +1496,7 @@ __global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const u
     const int msz = live ? R.msz() : 0;
     const int wmsz = max(wave_max(msz), 1);
     EncState16 S;
-    const bool ok = live && build_r16(R, msz, wmsz, S);
+    const bool ok = live && build_r16(R, msz, wmsz, S, hp);
     if (ok) {
       BitWriter bw;
       bw.out = oslots + (size_t)g * kSlotWords;
