@@ -199,6 +199,14 @@ constexpr uint32_t kWideGrid = MYYUV_WIDE_GRID;  // workgroups of k_huff_encode_
 #define MYYUV_R16_GATE (MYYUV_WIDE_GRID * MYYUV_WIDE_LANES)
 #endif
 constexpr uint32_t kR16Gate = MYYUV_R16_GATE;
+// Single frames: past two rounds of k_huff_encode_wave (a wave per block,
+// ~25 us a round), the tier and then the wave pass over what it leaves
+// (8192^2 q50: 55 + 26 us against 94 us in one CAP-64 lane round;
+// chef-big q90: 50 + 35 against 98 us in the wave pass; profiles/r6n_*).
+#ifndef MYYUV_R16_GATE_SINGLE
+#define MYYUV_R16_GATE_SINGLE (2 * 8192)
+#endif
+constexpr uint32_t kR16GateSingle = MYYUV_R16_GATE_SINGLE;
 constexpr uint32_t kR16Grid = 4096;  // workgroups of k_huff_encode_r16 (grid-stride, 64 blocks each)
 #ifndef MYYUV_K2_GROUP
 #define MYYUV_K2_GROUP 256

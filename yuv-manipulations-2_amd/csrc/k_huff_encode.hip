@@ -1466,7 +1466,7 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
 #define MYYUV_R16_LDS 1  // the heap in LDS (r16::LdsHeap16) rather than registers (r16::RegHeap16)
 #endif
 #ifndef MYYUV_R16_WAVES
-#define MYYUV_R16_WAVES 5  // waves per SIMD k_huff_encode_r16 is compiled for: 96 VGPRs, 8 spilled (3 waves at 131: -1.5 %, profiles/r3zzl_*)
+#define MYYUV_R16_WAVES 5  // waves per SIMD k_huff_encode_r16 is compiled for: 96 VGPRs, 12 spilled with the LDS heap (3 waves at 131: -1.5 %, profiles/r3zzl_*; no spills at 1 wave: no change alone, profiles/r6m_*)
 #endif
 __global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const uint4* __restrict__ coef,
                                                         const uint8_t* __restrict__ rmask,
@@ -1477,9 +1477,9 @@ __global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const u
                                                         const uint32_t* __restrict__ work,
                                                         const uint32_t* __restrict__ work_count,
                                                         uint32_t* __restrict__ work2,
-                                                        uint32_t* __restrict__ work2_count) {
+                                                        uint32_t* __restrict__ work2_count, uint32_t gate) {
   const uint32_t cnt = *work_count;
-  if (cnt <= kR16Gate) return;  // one CAP-64 round takes the list
+  if (cnt <= gate) return;  // short lists: the wave / lane passes take them whole
   const uint32_t lane = threadIdx.x;
 #if MYYUV_R16_LDS
   __shared__ uint32_t heap[16 * kWave];  // the lanes' heaps, one LDS column each

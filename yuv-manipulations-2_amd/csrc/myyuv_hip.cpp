@@ -47,7 +47,7 @@ __global__ void k_huff_encode_wide(const uint4*, const uint8_t*, const uint4*, F
                                    uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                    uint32_t, uint32_t);
 __global__ void k_huff_encode_r16(const uint4*, const uint8_t*, const uint4*, FrameGeom, uint32_t*, uint8_t*,
-                                  uint32_t*, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*);
+                                  uint32_t*, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t);
 __global__ void k_encode_tile(const uint8_t*, FrameGeom, const QTables*, uint4*, uint8_t*, uint32_t*, uint32_t*,
                               uint8_t*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_tile_scan(uint32_t*, FrameGeom, uint8_t*, uint32_t, uint32_t*, unsigned long long*);
@@ -410,7 +410,8 @@ uint32_t next_epoch(myyuv_hip_ctx* c) {
 // returns at once outside its regime.  A batch (nf > 1) takes the
 // lane-per-block pass only: its list is long, and the wave pass's per-block
 // SALU cost would crowd the other launch groups in flight (tools/kskip.py).
-// A list longer than one resident round of the lane pass (kR16Gate) goes
+// A list longer than one resident round of the lane pass (kR16Gate; a
+// single frame's: two rounds of the wave pass, kR16GateSingle) goes
 // through the CAP-16 register tier first (k_huff_encode_r16), and the two
 // passes then take what it leaves (more than 16 symbols: work[1] blocks from
 // word 64 + nblk).  work[0] is zeroed by K1 (or the host), work[1] here.
@@ -439,7 +440,8 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
   uint32_t* list2 = list + nblk;
   const uint32_t limit = nf > 1 ? kBatchWaveLimit : kWaveEncodeLimit;
   int e = 0;
-  const uint32_t gate = (nf == 1 || MYYUV_R16_BATCH) && nblk > kR16Gate ? kR16Gate : ~0u;
+  const uint32_t g16 = nf == 1 ? kR16GateSingle : kR16Gate;
+  const uint32_t gate = (nf == 1 || MYYUV_R16_BATCH) && nblk > g16 ? g16 : ~0u;
   // (launched whenever such a list is possible; with 8-frame launch groups,
   // whose lists stay below the gate, the empty launch cost 3.4 % of the
   // bench, profiles/r3zw_*; the bench's 24-frame groups take the tier)
@@ -451,7 +453,7 @@ int launch_overflow(myyuv_hip_ctx* c, const FrameGeom& G, hipStream_t s) {
     e |= launch(c, MYYUV_K_HUFF_R16, k_huff_encode_r16, dim3(r16), dim3(kWave), s, c->coef.as<const uint4>(),
                 c->rmask.as<const uint8_t>(), c->zq.as<const uint4>(), G, c->oslots.as<uint32_t>(),
                 c->sizes.as<uint8_t>(), c->tinfo.as<uint32_t>(), (const uint32_t*)list, (const uint32_t*)count,
-                list2, count2);
+                list2, count2, gate);
   }
   if (limit > 0)
     e |= launch(c, MYYUV_K_HUFF_WAVE, k_huff_encode_wave, dim3(kWaveEncodeGrid), dim3(kWave), s,
