@@ -1,4 +1,4 @@
-// huff_r16.hpp — register-resident Huffman code construction for blocks with
+// huff_r16.hpp — lane-per-block Huffman code construction for blocks with
 // at most 16 distinct symbols, lane per block (the overflow tier behind K2's
 // CAP-8 encoder: natural images at q50 put 99.8 % of their overflow blocks
 // here, q90 94 %; SURVEY.md §7 hard part 2, App. B).  Same bytes as
@@ -14,10 +14,12 @@
 //      order: the same ordering rule over (previous walk order, later keys);
 //      each ordering is two 16-element sorting networks;
 //   3. the libstdc++ binary heap (push_heap, pop_heap = __adjust_heap +
-//      __push_heap) on 16 registers: a pop walks the smaller-child path down
-//      from the root and merges the old last element back into it, a push
-//      merges the new element into its ancestor chain; both are written as
-//      per-position selects over the (at most 5) path positions;
+//      __push_heap): in the kernel one LDS column per lane (LdsHeap16, the
+//      walks as plain per-lane loops, one round trip per level); on the host
+//      and as the reference form on 16 registers (RegHeap16: a pop walks the
+//      smaller-child path down from the root and merges the old last element
+//      back into it, a push merges the new element into its ancestor chain,
+//      both as per-position selects over the path positions);
 //   4. depths, lengths, canonical order (a sorting network), codes, table;
 //   5. emission into the block's 160-B overflow slot.
 // Compiled for the host as well (MYYUV_HD) and checked against the oracle on
