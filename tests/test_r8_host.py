@@ -60,10 +60,23 @@ def run(exe, nat, mode):
     return res
 
 
+OVF_NUB = 16  # codec_common.hpp kOvfNub
+
+
+def ovf_class(msg, m):
+    """class_of's ovf class (codec_common.hpp): at least OVF_NUB symbol slots
+    (nonzero coefficients, plus one for a zero inside the message), sent to
+    the overflow worklist without a CAP-8 build."""
+    nnz = int(np.count_nonzero(msg[:m]))
+    nub = nnz + (1 if m > nnz else 0)
+    return m > 1 and nub >= OVF_NUB
+
+
 def check(exe, oracle, nat):
     """Every mode: build_r<4>, build_r<8> (each + emit_chunk), and the
     kernel's class dispatch ("auto", which adds build_single).  A block is
-    declined exactly when it has more distinct symbols than the CAP."""
+    declined exactly when it has more distinct symbols than the CAP, or
+    ("auto") when its class is ovf."""
     nat = np.asarray(nat, np.int16).reshape(-1, 64)
     n_ok = 0
     for mode, cap in (("4", 4), ("8", 8), ("auto", 8)):
@@ -73,12 +86,12 @@ def check(exe, oracle, nat):
             nz = np.nonzero(msg)[0]
             m = nz[-1] + 1 if len(nz) else 1
             distinct = len(set(msg[:m].tolist()))
-            if distinct > cap:
+            if distinct > cap or (mode == "auto" and ovf_class(msg, m)):
                 assert ch is None
                 continue
             assert ch == bytes(oracle.huff_encode_block(x)), (mode, msg[:m])
-            n_ok += mode == "auto"
-    return n_ok
+            n_ok += mode == "8"
+    return n_ok  # (blocks build_r<8> encoded)
 
 
 def test_r8_edge_blocks(harness, oracle):
@@ -137,7 +150,7 @@ def test_dense_run_matches_concatenated_chunks(harness, oracle):
         msg = x[ZZ]
         nz = np.nonzero(msg)[0]
         m = nz[-1] + 1 if len(nz) else 1
-        if len(set(msg[:m].tolist())) <= 8:
+        if len(set(msg[:m].tolist())) <= 8 and not ovf_class(msg, m):
             want += bytes(oracle.huff_encode_block(x))
     assert total == len(want)
     assert out[4:] == want

@@ -42,6 +42,7 @@ static bool build(const CoefRegs& R, const char* mode, EncState& S) {
   if (mode[0] == '4') return build_r<4>(R, msz, 64, S);
   if (mode[0] == '8') return build_r<8>(R, msz, 64, S);
   const uint32_t cls = block_class(R, msz);
+  if (cls == kClassOvf) return false;  // straight to the overflow worklist
   if (cls == kClassSingle) {
     build_single(R, S);
     return true;

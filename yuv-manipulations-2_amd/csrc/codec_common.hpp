@@ -74,13 +74,21 @@ constexpr int kMaxChunk = 160;
 // wave runs the cheapest encoder that fits all its blocks):
 //   single: msz <= 1, one symbol;  r4 / r8: at most 4 / 8 distinct symbols
 //   for sure (nonzero coefficients, plus one for a zero inside the message);
-//   r8x: the rest, encode_block_r<8> with the overflow worklist behind it.
+//   r8x: up to kOvfNub - 1 such symbol slots, encode_block_r<8> with the
+//   overflow worklist behind it;  ovf: kOvfNub or more, straight to the
+//   overflow worklist (K2 builds nothing for them: of the bench frame's
+//   blocks with 16 or more, 10 % fit 8 distinct symbols, and they carry the
+//   longest messages: msz 23-50; the CAP-16 tier takes them whole).
 // msz = 1 + zig-zag index of the last nonzero coefficient (0: all zero).
-constexpr uint32_t kClassSingle = 0, kClassR4 = 1, kClassR8 = 2, kClassR8x = 3, kClassDead = 4;
+constexpr uint32_t kClassSingle = 0, kClassR4 = 1, kClassR8 = 2, kClassR8x = 3, kClassOvf = 4, kClassDead = 5;
+#ifndef MYYUV_OVF_NUB
+#define MYYUV_OVF_NUB 16  // (65: no block is of the ovf class)
+#endif
+constexpr uint32_t kOvfNub = MYYUV_OVF_NUB;
 __host__ __device__ __forceinline__ uint32_t class_of(uint32_t nnz, uint32_t msz) {
   if (msz <= 1) return kClassSingle;
   const uint32_t nub = nnz + (msz > nnz ? 1u : 0u);
-  return nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : kClassR8x);
+  return nub <= 4 ? kClassR4 : (nub <= 8 ? kClassR8 : (nub < kOvfNub ? kClassR8x : kClassOvf));
 }
 // Natural coefficient pair w (coefficients 2w, 2w+1): (zig-zag index + 1) of
 // each, in the two 16-bit halves.

@@ -895,12 +895,13 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
   const uint32_t mc = sc.cls[e];
   const uint32_t mrm = sc.rm[e];
   const bool live = mc != kClassDead;
+  const bool bld = live && mc != kClassOvf;  // (ovf blocks: straight to the worklist)
   const uint32_t mg = gb + ml;
-  uint32_t wcls = kClassDead;  // the wave's heaviest live class
+  uint32_t wcls = kClassDead;  // the wave's heaviest class to build
 #pragma unroll
-  for (int c = kClassDead - 1; c >= 0; c--)
+  for (int c = kClassOvf - 1; c >= 0; c--)
     if (wcls == kClassDead && __ballot(mc == (uint32_t)c) != 0) wcls = (uint32_t)c;
-  const int wmsz = max(wave_max(live ? mm : 0), 1);
+  const int wmsz = max(wave_max(bld ? mm : 0), 1);
 #ifdef MYYUV_STAMPS
   const uint32_t wid = T * kWaves + wave;
   if (lane == 0 && wid < 8192) g_k2_fstamps[wid * 8 + 0] = wcls | ((uint32_t)wmsz << 8);
@@ -908,18 +909,18 @@ __device__ __forceinline__ void encode_tile(const Src& src, TileScratch& sc, uin
 #endif
   EncState S;
   bool ok = false;
-  if (wcls != kClassDead) {
+  if (__ballot(live) != 0) {
     CoefRegs R;
     src.load(R, live ? ml : 0u, live ? mrm : 0u);
     if (wcls == kClassSingle) {
-      if (live) {
+      if (bld) {
         build_single(R, S);
         ok = true;
       }
     } else if (wcls == kClassR4) {
-      if (live) ok = build_r<4>(R, mm, wmsz, S);
-    } else {
-      if (live) ok = build_r<8>(R, mm, wmsz, S);
+      if (bld) ok = build_r<4>(R, mm, wmsz, S);
+    } else if (wcls != kClassDead) {
+      if (bld) ok = build_r<8>(R, mm, wmsz, S);
     }
     if (live && !ok) src.spill(R, ml, mrm);
   }
@@ -1209,13 +1210,14 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     const uint32_t mc = sc.cls[e];
     const uint32_t mrm = sc.rm[e];
     const bool live = e < nlive;
+    const bool bld = live && mc != kClassOvf;  // (ovf blocks: straight to the worklist)
     const uint32_t k = sl >> 8;
     const uint32_t mg = sc.gb[k] + (sl & 255u);
-    uint32_t wcls = kClassDead;  // the run's heaviest class
+    uint32_t wcls = kClassDead;  // the run's heaviest class to build
 #pragma unroll
-    for (int c = kClassDead - 1; c >= 0; c--)
-      if (wcls == kClassDead && __ballot(live && mc == (uint32_t)c) != 0) wcls = (uint32_t)c;
-    const int wmsz = max(wave_max_full(live ? mm : 0), 1);
+    for (int c = kClassOvf - 1; c >= 0; c--)
+      if (wcls == kClassDead && __ballot(bld && mc == (uint32_t)c) != 0) wcls = (uint32_t)c;
+    const int wmsz = max(wave_max_full(bld ? mm : 0), 1);
     EncState S;
     bool ok = false;
     // (the coefficients are loaded inside each class's branch: loaded before
@@ -1224,19 +1226,19 @@ __global__ __launch_bounds__(kK2Group, MYYUV_K2_WAVES) void k_huff_encode(const 
     if (wcls == kClassSingle) {
       // one symbol: the DC coefficient (word 0 of quad 0), or 0
       // (single-class runs take the DC from LDS, kept at classification, not from HBM)
-      const uint32_t dc = live ? (uint32_t)sc.dc[sl] : 0u;
-      if (live) {
+      const uint32_t dc = bld ? (uint32_t)sc.dc[sl] : 0u;
+      if (bld) {
         build_single_dc((int)(int16_t)dc, S);
         ok = true;
       }
     } else if (wcls == kClassR4) {
       CoefRegs R;
-      R.load(coef, zq, live ? mg : 0u, live ? mrm : 0u);
-      if (live) ok = build_r<4>(R, mm, wmsz, S);
-    } else {
+      R.load(coef, zq, bld ? mg : 0u, bld ? mrm : 0u);
+      if (bld) ok = build_r<4>(R, mm, wmsz, S);
+    } else if (wcls != kClassDead) {
       CoefRegs R;
-      R.load(coef, zq, live ? mg : 0u, live ? mrm : 0u);
-      if (live) ok = build_r<8>(R, mm, wmsz, S);
+      R.load(coef, zq, bld ? mg : 0u, bld ? mrm : 0u);
+      if (bld) ok = build_r<8>(R, mm, wmsz, S);
     }
 #ifdef MYYUV_STAMPS
     KWSTAMP(1);
