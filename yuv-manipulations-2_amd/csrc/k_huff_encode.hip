@@ -973,19 +973,29 @@ namespace {
 // kWinTiles or kWinTilesBig, k2_win).  Sort slots are the (tile round, wave)
 // pairs that classified them, so the order is stable: class, then window slot
 // (tile, block).
-// sort keys: the single class, then each of the other classes split by
-// message length (<= 8, <= 16, longer: the per-position loops run to the
-// run's longest message), the dead slots last
+// sort keys: the single class, then each class K2 builds (r4, r8, r8x)
+// split by message length (the per-position loops run to the run's longest
+// message), then the ovf class (built by the overflow passes: one key), the
+// dead slots last.  Length buckets (MYYUV_K2_MSZ_SPLIT): 2 -> <= 8, <= 16,
+// longer (rounds 3-5); 3 -> <= 6, <= 12, <= 20, longer (round 6: the sum of
+// the runs' longest messages over the bench frame 28.2k -> 26.4k,
+// tools/diag/k2_run_sim.py)
 #ifndef MYYUV_K2_MSZ_SPLIT
-#define MYYUV_K2_MSZ_SPLIT 1
+#define MYYUV_K2_MSZ_SPLIT 3
 #endif
-constexpr uint32_t kMszBuckets = MYYUV_K2_MSZ_SPLIT ? 3 : 1;
-constexpr uint32_t kKeys = 2 + (kClassDead - 1) * kMszBuckets;
+constexpr uint32_t kMszBuckets = MYYUV_K2_MSZ_SPLIT + 1;
+constexpr uint32_t kOvfKey = 1 + (kClassOvf - 1) * kMszBuckets;
+constexpr uint32_t kKeys = kOvfKey + 2;
 constexpr uint32_t kDeadKey = kKeys - 1;
 __device__ __forceinline__ uint32_t sort_key(uint32_t cls, uint32_t msz) {
   if (cls == kClassDead) return kDeadKey;
+  if (cls == kClassOvf) return kOvfKey;
   if (cls == kClassSingle) return 0;
-  const uint32_t b = kMszBuckets == 1 ? 0u : (msz > 8 ? 1u : 0u) + (msz > 16 ? 1u : 0u);
+  uint32_t b;
+  if constexpr (MYYUV_K2_MSZ_SPLIT == 3)
+    b = (msz > 6 ? 1u : 0u) + (msz > 12 ? 1u : 0u) + (msz > 20 ? 1u : 0u);
+  else
+    b = (msz > 8 ? 1u : 0u) + (msz > 16 ? 1u : 0u);
   return 1 + (cls - 1) * kMszBuckets + b;
 }
 template <uint32_t W>
