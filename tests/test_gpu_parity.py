@@ -127,8 +127,10 @@ def test_fdct_unproven_units_listed_in_batches(oracle, q, fix_grid):
 @pytest.mark.parametrize("q", [(50, 50, 50), (100, 100, 100)])
 def test_noise_long_overflow_list(codec, oracle, q):
     """A noise frame whose blocks nearly all exceed 8 distinct symbols: the
-    overflow worklist is longer than kWaveEncodeLimit (24576), so K2 takes the
-    lane-per-block overflow pass instead of the wave-per-block one."""
+    single frame's overflow worklist is longer than kR16GateSingle (16,384),
+    so the CAP-16 tier (k_huff_encode_r16) takes it first, and the blocks with
+    more than 16 distinct symbols it leaves go to the wave pass (at most
+    kWaveEncodeLimit, 24,576, of them) or the lane-per-block CAP-64 pass."""
     import synth
     w, h = 2048, 1024  # 49,152 blocks
     fr = synth.noise_frame(w, h)
