@@ -5,11 +5,11 @@ Workloads (--workload; `auto`, the default, is chef-big at every rank count,
 so the driver's 1/2/4/8-GPU runs form one weak-scaling curve of one workload):
   chef-big  BASELINE.json configs[1], the metric's own configuration: a step
             is one DCT compress + decompress round trip of --inflight x
-            --batch (default 4 x 24 = 96) 4032x3008 IYUV frames per rank
+            --batch (default 4 x 32 = 128) 4032x3008 IYUV frames per rank
             (chef-with-trumpet-big, q=50; its raw input is missing from the
             reference, so the frame is the sha-pinned decode of
             chef-with-trumpet-big-DCT-50.myyuv), read from --input-frames
-            (default: one per frame of a step, at least 24, rounded down to a
+            (default: one per frame of a step, at least 32, rounded down to a
             multiple of --batch) distinct HBM copies: more bytes than the 256
             MiB Infinity Cache, so the pixel reads come from HBM.  Weak scaling: every rank runs that batch,
             and at N > 1 every rank's compressed streams are gathered to rank 0
@@ -152,7 +152,7 @@ def parse(argv=None):
                     help="launch groups in flight per GPU, each on its own codec context and HIP stream "
                          "(1 = strictly serial; 0 = 4)")
     ap.add_argument("--batch", type=int, default=0,
-                    help="frames per launch (the batch entry points; 0 = 24)")
+                    help="frames per launch (the batch entry points; 0 = 32 for chef-big, 24 for batch4k)")
     ap.add_argument("--stream-priority", default="",
                     help="comma-separated HIP stream priorities of the launch groups' streams "
                          "(cycled; default all normal)")
@@ -168,8 +168,8 @@ def parse(argv=None):
                     help="untimed launch groups after the timed region with every kernel stamped")
     ap.add_argument("--input-frames", type=int, default=0,
                     help="chef-big: distinct HBM copies of the input frame the launch groups read in turn "
-                         "(0: one per frame of a step, at least 24; rounded down to a multiple of --batch: "
-                         "96 copies, 1.75 GB at the default 4 x 24, larger than the 256 MiB Infinity Cache)")
+                         "(0: one per frame of a step, at least 32; rounded down to a multiple of --batch: "
+                         "128 copies, 2.33 GB at the default 4 x 32, larger than the 256 MiB Infinity Cache)")
     ap.add_argument("--cpu-codec", action="store_true",
                     help="tests only: the CPU restatement as the codec, host tensors, gloo (no GPU)")
     ap.add_argument("--cpu-codec-fail", default="",
@@ -523,12 +523,12 @@ class Run:
         self.verified = {}
         if name == "chef-big":
             self.w, self.h = big.width, big.height
-            self.B = args.batch or 24
+            self.B = args.batch or 32
             self.per_step = self.nf * self.B
             self.n_local = self.per_step
             self.n_total = world * self.per_step
             self.cap = SLOT_4K if isinstance(codec, CpuCodec) else None
-            want = args.input_frames or max(24, self.per_step)
+            want = args.input_frames or max(32, self.per_step)
             nin = max(self.B, (max(want, self.B) // self.B) * self.B)
             self.nin = nin
             self.samples = self.w * self.h * 3 // 2
@@ -941,11 +941,12 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     name = args.workload if args.workload != "auto" else "chef-big"
     dist = None
-    # launch shape 4 x 24: the launch groups' overflow lists (~200k blocks) take the CAP-16 tier
+    # launch shape (4 x 32 since round 6; 4 x 24 before): the launch groups' overflow lists (~200k blocks) take the CAP-16 tier
     # (round 3: 3 x 24 264.2k against 233.1k MP/s for 4 x 8, flat from 3 x 24 to 3 x 48,
     # profiles/r3zzf_*, r3zzg_*); with round 4's K1, 4 x 24 288.1k / 292.2k against 3 x 24
     # 282.6k / 287.0k at 20 / 40 steps, 5 streams slower (one per hardware queue: 4),
-    # profiles/r4j_launch_shapes.txt
+    # profiles/r4j_launch_shapes.txt; round 6 (with K2's ovf class): 4 x 32 356.3k / 357.1k against
+    # 4 x 24 351.0k / 352.6k, 4 x 40 354.6k, 4 x 48 354.0k, 3 x 32 351.5k (profiles/r6ac_*, r6ad_*)
     nf = max(1, args.inflight or 4)
     prios = [int(v) for v in args.stream_priority.split(",")] if args.stream_priority else [0]
     big = myyuv_file.YUVFile.load(GOLDEN_BIG)
