@@ -1478,7 +1478,7 @@ __global__ __launch_bounds__(kWideLanes) void k_huff_encode_wide(const uint4* __
 #define MYYUV_R16_LDS 1  // the heap in LDS (r16::LdsHeap16) rather than registers (r16::RegHeap16)
 #endif
 #ifndef MYYUV_R16_WAVES
-#define MYYUV_R16_WAVES 5  // waves per SIMD k_huff_encode_r16 is compiled for: 96 VGPRs, 12 spilled with the LDS heap (3 waves at 131: -1.5 %, profiles/r3zzl_*; no spills at 1 wave: no change alone, profiles/r6m_*)
+#define MYYUV_R16_WAVES 5  // waves per SIMD k_huff_encode_r16 is compiled for: 96 VGPRs, 12 spilled with the LDS heap (4 waves, 128 VGPRs, none spilled: 106 against 129 us alone per 32-frame launch but the bench -0.9 %, profiles/r6ag_*; 3 waves: -1.5 %, r3zzl_*)
 #endif
 __global__ __launch_bounds__(64, MYYUV_R16_WAVES) void k_huff_encode_r16(const uint4* __restrict__ coef,
                                                         const uint8_t* __restrict__ rmask,
