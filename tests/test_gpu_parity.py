@@ -524,3 +524,40 @@ def test_device_compress_capacity_is_respected(codec, golden, oracle, cap):
     assert int(d_size.item()) == len(want)
     tail = d_pay[cap:].cpu()
     assert bool((tail == 0xA5).all())
+
+
+def sweep_frame(w, h, rng, sigma=None):
+    """A smooth random gradient plus Gaussian noise of a random strength (0 to
+    48), optionally quantised to a few levels: from DC-only blocks through
+    every K2 class to noise whose blocks nearly all overflow (a 1024x1024
+    frame of it passes the CAP-16 tier's single-frame gate)."""
+    out = []
+    sigma = float(rng.choice([0.0, 2.0, 6.0, 16.0, 48.0])) if sigma is None else sigma
+    levels = int(rng.choice([0, 0, 4, 16]))
+    for pw, ph in ((w, h), (w // 2, h // 2), (w // 2, h // 2)):
+        y, x = np.mgrid[0:ph, 0:pw]
+        a, b, c = rng.uniform(-1.5, 1.5, 3)
+        img = 128 + a * (x - pw / 2) * 64 / max(pw, 1) + b * (y - ph / 2) * 64 / max(ph, 1) \
+            + c * 40 * np.sin(x / 7.0 + y / 11.0) + rng.normal(0, sigma, (ph, pw))
+        if levels:
+            img = np.round(img / (256 / levels)) * (256 / levels)
+        out.append(np.clip(np.rint(img), 0, 255).astype(np.uint8).reshape(-1))
+    return np.concatenate(out).tobytes()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_sweep_vs_oracle(codec, oracle, seed):
+    """Seeded random geometries (multiples of 16 up to 1024), per-plane
+    qualities (1..100) and content (sweep_frame): stream and decode equal the
+    oracle's."""
+    rng = np.random.default_rng(1000 + seed)
+    w, h = (int(v) * 16 for v in rng.integers(1, 65, 2))
+    q = tuple(int(v) for v in rng.integers(1, 101, 3))
+    sigma = None
+    if seed % 4 == 0:  # strong noise over 1024x1024: a single-frame overflow list past the tier's gate
+        w, h, sigma = 1024, 1024, 48.0
+        q = tuple(max(v, 40) for v in q)
+    fr = sweep_frame(w, h, rng, sigma)
+    pay = oracle.compress(fr, w, h, q)
+    assert codec.compress(fr, w, h, q) == pay, (w, h, q)
+    assert codec.decompress(pay, w, h, q) == oracle.decompress(pay, w, h, q), (w, h, q)
